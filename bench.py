@@ -1,0 +1,218 @@
+"""bench.py — env-steps/s of beergame-v0 at 65,536 envs per GPU (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A "step" is one BeerGameVecEnv.step() over this rank's 65,536 envs: one fused HIP step
+kernel through the C ABI (include/scgpu.h) — receive, order slips, fill, ship, backlog,
+orders, observation, reward, cost ledgers, order history and episode return, with
+Poisson(8) demand drawn on device (Philox4x32-10) and auto-reset at week 35. Actions are
+synthetic uniform integers in [0, 8], generated on device before timing (the policy's
+output, resident in HBM). Envs shard across ranks by global id; the only collective is the
+async RCCL all-gather of per-env episode returns at each episode end.
+
+Rank 0 prints ONE JSON line. `roofline` prices the step kernel: algorithmic bytes per
+launch (DESIGN.md §Roofline, 260 B per env on a regular week) ÷ the kernel's average
+duration from HIP events recorded around every launch of the timed region on the launch
+stream. `cpu_baseline` times oracle.beergame.BeerGameOracle — the per-env NumPy
+restatement of the reference step() — on the host's cores (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "gym-supplychain_amd"))
+sys.path.insert(0, REPO)
+
+N_ENVS = 65536
+LEVELS = 4
+WEEKS = 35
+LAMBDA = 8.0
+SEED = 0x5EED0000
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
+
+
+def step_bytes_per_env(plan_word, week, T, L, ring_initial_slots, ledgers, history, returns, autoreset):
+    """Algorithmic HBM bytes one env moves in one bg_step_kernel launch (mirrors the kernel).
+
+    Regular week of the bench config (due row arrives, scheduled row stored, ledgers,
+    history and returns on): 4 rows in (action, inventory, backlog, orders) + due row +
+    scheduled row + history row + 4 rows out (state, obs) + 2 ledger rows RMW + reward
+    + episode return RMW = 64+16+16+16+64+64+4+16 = 260 B at L = 4.
+    """
+    row = 4 * L
+    mode, arrive = plan_word & 3, bool(plan_word & 4)
+    terminal = week == T
+    b = 4 * row + 4                                 # action/inventory/backlog/orders in, reward out
+    b += row if arrive else 0                       # due pipeline row in
+    b += {0: 0, 1: row, 2: 2 * row, 3: 0}[mode]     # scheduled row: store / read-modify-write
+    b += row if history else 0                      # all_orders_placed row out
+    b += row if terminal else 0                     # terminal observation out
+    if returns:
+        b += 16 + (8 if terminal else 0)            # episode return RMW, final return out
+    if terminal and autoreset:                      # reset in the same launch
+        b += 3 * row + ring_initial_slots * row + row
+        b += 2 * row if ledgers else 0
+        b += row if history else 0
+    else:
+        b += 4 * row                                # inventory/backlog/orders/obs out
+        b += 4 * row if ledgers else 0              # two ledger rows read + write
+    return b
+
+
+def cpu_baseline(budget_s=1.5, max_procs=16):
+    """Per-env NumPy restatement of BeerGameEnv.step on the host's cores (oracle, 'port')."""
+    import multiprocessing as mp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    procs = max(1, min(max_procs, cores))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(i, budget_s) for i in range(procs)])
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} processes x {budget_s:.1f} s of beergame-v0 episodes (35 weeks, Poisson(8) "
+                      f"demand, uniform [0,8] actions), one env per process, oracle.beergame.BeerGameOracle; "
+                      f"{steps} env-steps total"}
+
+
+def _cpu_worker(arg):
+    idx, budget_s = arg
+    import numpy as np
+    sys.path.insert(0, REPO)
+    from oracle.beergame import BeerGameOracle
+    from oracle.philox import STREAM_DEMAND, draw_words
+    from oracle.poisson import poisson_invert, poisson_thresholds
+    thr = poisson_thresholds(LAMBDA)
+    rng = np.random.RandomState(idx)
+    steps, ep = 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        demand = poisson_invert(draw_words(SEED, [idx], ep, WEEKS, STREAM_DEMAND), thr)[0]
+        acts = rng.randint(0, 9, size=(WEEKS, LEVELS))
+        env = BeerGameOracle({"customer_demand": demand.tolist()})
+        env.reset()
+        for w in range(WEEKS):
+            env.step(acts[w])
+        steps += WEEKS
+        ep += 1
+    return steps, time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3500)
+    ap.add_argument("--warmup", type=int, default=350)
+    ap.add_argument("--envs", type=int, default=N_ENVS, help="envs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=1.5)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    import ctypes
+
+    from gym_supplychain_amd import BeerGameVecEnv
+    from gym_supplychain_amd import _native as nat
+    from gym_supplychain_amd.distributed import EpisodeReturnGather, shard_offset
+
+    N = args.envs
+    env = BeerGameVecEnv(N, {}, demand="poisson", poisson_lambda=LAMBDA, seed=SEED, device=device,
+                         env_offset=shard_offset(N, rank), auto_reset=True, track_costs=True,
+                         track_history=True, track_returns=True)
+    stream = torch.cuda.current_stream(device)
+    actions = torch.empty((WEEKS, N, LEVELS), dtype=torch.int32, device=device)
+    nat.check(nat.lib.scg_uniform_ints(SEED, env.env_offset, N, WEEKS, LEVELS, 0, 0, 8, actions.data_ptr(),
+                                       ctypes.c_void_p(stream.cuda_stream)))
+    gather = EpisodeReturnGather(N, device)
+    env.reset()
+
+    def run(k, events=None):
+        for i in range(k):
+            w = env.week
+            if events is not None:
+                events[i][0].record(stream)
+            _, _, done, info = env.step(actions[w])
+            if events is not None:
+                events[i][1].record(stream)
+            if info:
+                gather.on_episode_end(info["episode_return"])
+
+    run(args.warmup)
+    # byte accounting for the weeks the timed region will cover (lock-step, known on host)
+    plan = list(env._plan)
+    w0 = env.week
+    total_bytes = 0
+    for i in range(args.steps):
+        w = (w0 + i) % WEEKS + 1
+        total_bytes += N * step_bytes_per_env(plan[w], w, WEEKS, LEVELS, 2, True, True, True, True)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps, events)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gather.result()
+    torch.cuda.synchronize()
+    kern_ms = sum(s.elapsed_time(e) for s, e in events)
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        value = N * world * args.steps / elapsed
+        avg_kernel_s = kern_ms / 1e3 / args.steps
+        achieved = total_bytes / args.steps / avg_kernel_s / 1e9
+        line = {
+            "metric": "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: Poisson(8) demand drawn on device (Philox4x32-10), uniform int [0,8] actions",
+            "config": {"workload": "beergame-v0 step() x 65536 envs/GPU (BASELINE configs[1]; configs[4] at N=8)",
+                       "n_envs_per_gpu": N, "levels": LEVELS, "weeks": WEEKS, "auto_reset": True,
+                       "ledgers": True, "orders_history": True, "episode_return_allgather": world > 1,
+                       "parallelism": f"env-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "scg::bg_step_kernel<4>", "avg_kernel_us": avg_kernel_s * 1e6,
+                         "bytes_per_launch": total_bytes / args.steps},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,655 @@
+// BeerGame hot path for gfx950: reset / step / rollout kernels + their C-ABI launchers.
+//
+// Reference: gym_supplychain/envs/beergame_env.py (BeerGameEnv), snapshot 2024-08-07.
+// One lane owns one env for the whole launch; every per-env array is env-major [N][L]
+// int32, so for the default L = 4 each state row is one 16-byte global_load_dwordx4 /
+// global_store_dwordx4 per lane and a wavefront moves 1 KiB per instruction, fully
+// coalesced. The path is HBM/launch bound integer work (≈35 int ops per env-step);
+// there is no contraction, so no MFMA and no LDS tiling — see DESIGN.md.
+//
+// The reference keeps an absolute-week shipment table (beergame_env.py:46-52) that is
+// never shifted (:73-74). Here it is a ring of R = max delay + 1 week slots; the host
+// plan (scg_bg_prepare) decides per week whether the due slot holds deliveries and
+// whether the scheduled slot is written fresh (store) or accumulated (read-modify-write),
+// so the common constant-delay case moves exactly one due row in and one row out.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "scg_philox.h"
+#include "scgpu.h"
+
+namespace scg {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(SCG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return SCG_OK;
+}
+
+// ---- per-week plan word (host computed, uniform per launch) -------------------------
+enum : int32_t { MODE_DIRECT = 0, MODE_STORE = 1, MODE_ADD = 2, MODE_DROP = 3 };
+constexpr int32_t PLAN_ARRIVE = 4;
+inline int32_t plan_mode(int32_t p) { return p & 3; }
+inline bool plan_arrive(int32_t p) { return (p & PLAN_ARRIVE) != 0; }
+inline int32_t plan_delay(int32_t p) { return (p >> 8) & 0xff; }
+
+constexpr int kBlock = 256;
+
+// ---- kernel arguments (passed by value, ≈300 B of the 4 KiB argument segment) -------
+struct BgArgs {
+  int32_t* inv;
+  int32_t* bk;
+  int32_t* op;
+  int32_t* ring;
+  int32_t* inv_acc;
+  int32_t* bk_acc;
+  int32_t* hist;
+  int64_t* ep_ret;
+  int64_t* final_ret;
+  const int32_t* act;
+  int32_t* obs;
+  int32_t* rew;
+  int32_t* term_obs;
+  const int32_t* demand_table;
+  const uint32_t* pthr;
+  int64_t n;           // envs in this shard
+  int64_t env_offset;  // global id of env 0
+  uint32_t key0, key1;
+  uint32_t episode;
+  int32_t demand_mode;
+  int32_t pthr_len;
+  int32_t h, b;        // inv_cost, backlog_cost
+  int32_t ship_value, orders_value;
+  int32_t init_slots;  // weeks 1..init_slots hold the initial pipeline (:52)
+  int32_t ring_slots;
+  int32_t init_inv[SCG_BG_MAX_LEVELS];
+};
+
+// ---- row helpers: L contiguous int32 per env, widest aligned vector access ----------
+template <int L>
+__device__ __forceinline__ void load_row(const int32_t* __restrict__ p, int32_t (&v)[L]) {
+  if constexpr (L % 4 == 0) {
+#pragma unroll
+    for (int c = 0; c < L / 4; ++c) {
+      const int4 t = reinterpret_cast<const int4*>(p)[c];
+      v[4 * c] = t.x; v[4 * c + 1] = t.y; v[4 * c + 2] = t.z; v[4 * c + 3] = t.w;
+    }
+  } else if constexpr (L % 2 == 0) {
+#pragma unroll
+    for (int c = 0; c < L / 2; ++c) {
+      const int2 t = reinterpret_cast<const int2*>(p)[c];
+      v[2 * c] = t.x; v[2 * c + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int l = 0; l < L; ++l) v[l] = p[l];
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void store_row(int32_t* __restrict__ p, const int32_t (&v)[L]) {
+  if constexpr (L % 4 == 0) {
+#pragma unroll
+    for (int c = 0; c < L / 4; ++c)
+      reinterpret_cast<int4*>(p)[c] = make_int4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+  } else if constexpr (L % 2 == 0) {
+#pragma unroll
+    for (int c = 0; c < L / 2; ++c) reinterpret_cast<int2*>(p)[c] = make_int2(v[2 * c], v[2 * c + 1]);
+  } else {
+#pragma unroll
+    for (int l = 0; l < L; ++l) p[l] = v[l];
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void fill_row(int32_t* __restrict__ p, int32_t x) {
+  int32_t v[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) v[l] = x;
+  store_row<L>(p, v);
+}
+
+// Customer demand of env n for `week` (1-based): beergame_env.py:79 reads
+// customer_demand[week-1]; here per env from a table (TABLE) or drawn on device
+// (POISSON). The shared FIXED list arrives as a per-week kernel argument instead.
+__device__ __forceinline__ int32_t week_demand(const BgArgs& a, int64_t n, int32_t week,
+                                               uint32_t episode) {
+  if (a.demand_mode == SCG_DEMAND_TABLE) return a.demand_table[(int64_t)(week - 1) * a.n + n];
+  const uint32_t u = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n),
+                                      episode, static_cast<uint32_t>(week - 1), SCG_STREAM_DEMAND);
+  // Inverse CDF on uint32 thresholds: #{k : thr[k] <= u}. The index is wave-uniform, so
+  // the table streams through scalar loads; no divergent search.
+  const uint32_t* __restrict__ thr = a.pthr;
+  int32_t x = 0;
+  for (int k = 0; k < a.pthr_len; ++k) x += (thr[k] <= u) ? 1 : 0;
+  return x;
+}
+
+// reset() of one env (beergame_env.py:140-156), writing the device state rows.
+template <int L>
+__device__ __forceinline__ void reset_env(const BgArgs& a, int64_t n, int32_t* __restrict__ obs_out) {
+  const int64_t row = n * L;
+  const int64_t stride = a.n * L;
+  int32_t inv[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) inv[l] = a.init_inv[l];
+  store_row<L>(a.inv + row, inv);
+  fill_row<L>(a.bk + row, 0);
+  fill_row<L>(a.op + row, a.orders_value);
+  for (int t = 1; t <= a.init_slots; ++t) fill_row<L>(a.ring + (t % a.ring_slots) * stride + row, a.ship_value);
+  if (a.inv_acc) fill_row<L>(a.inv_acc + row, 0);
+  if (a.bk_acc) fill_row<L>(a.bk_acc + row, 0);
+  if (a.hist) fill_row<L>(a.hist + row, a.orders_value);  // all_orders_placed[:, 0] (:152)
+  if (a.ep_ret) a.ep_ret[n] = 0;
+  if (obs_out) store_row<L>(obs_out + row, inv);            // inventory - backlog, backlog = 0
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void bg_reset_kernel(const BgArgs a) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= a.n) return;
+  reset_env<L>(a, n, a.obs);
+}
+
+// One week of one env (beergame_env.py:66-138) on registers. `ship` rows go to the ring
+// (or straight into inventory when the week's delay is 0). Shared by the step kernel
+// (state from/to HBM each launch) and the rollout kernel (state held in registers).
+struct WeekInfo {
+  int32_t week;        // 1..T
+  int32_t read_slot;   // -1: nothing due
+  int32_t write_slot;
+  int32_t mode;        // MODE_*
+  int32_t demand_fixed;
+  int32_t flags;       // bit0 terminal, bit1 autoreset
+};
+
+template <int L>
+__device__ __forceinline__ int32_t step_core(const BgArgs& a, int64_t n, const WeekInfo& wk, uint32_t episode,
+                                             int32_t (&inv)[L], int32_t (&bk)[L], int32_t (&op)[L],
+                                             const int32_t (&act)[L], int32_t (&obs)[L], int32_t (&ic)[L],
+                                             int32_t (&bc)[L]) {
+  const int64_t row = n * L;
+  const int64_t stride = a.n * L;
+  // 1. receive the shipments due this week (:72)
+  if (wk.read_slot >= 0) {
+    int32_t due[L];
+    load_row<L>(a.ring + wk.read_slot * stride + row, due);
+#pragma unroll
+    for (int l = 0; l < L; ++l) inv[l] += due[l];
+  }
+  // 2. order slips: customer demand at level 0, the previous orders above (:79-81)
+  int32_t inc[L];
+  inc[0] = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, episode);
+#pragma unroll
+  for (int l = 1; l < L; ++l) inc[l] = op[l - 1];
+  // fill what inventory allows (:85-89)
+  int32_t fill[L], del[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    fill[l] = inc[l] + bk[l];
+    del[l] = min(inv[l], fill[l]);
+  }
+  // ship downstream deliveries and the factory's previous order (:93-96, :111-114):
+  // ship[l] = what level l receives: deliver[l+1] from the level above it, and for the
+  // factory its own orders_placed[-1] from before this step.
+  int32_t ship[L];
+#pragma unroll
+  for (int l = 0; l + 1 < L; ++l) ship[l] = del[l + 1];
+  ship[L - 1] = op[L - 1];
+  if (wk.mode == MODE_DIRECT) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) inv[l] += ship[l];
+  } else if (wk.mode == MODE_STORE) {
+    store_row<L>(a.ring + wk.write_slot * stride + row, ship);
+  } else if (wk.mode == MODE_ADD) {
+    int32_t* p = a.ring + wk.write_slot * stride + row;
+    int32_t cur[L];
+    load_row<L>(p, cur);
+#pragma unroll
+    for (int l = 0; l < L; ++l) cur[l] += ship[l];
+    store_row<L>(p, cur);
+  }  // MODE_DROP: arrives after the horizon, never observable
+  // 3. inventory / backlog (:101-103); 5. place orders (:121); obs (:127,:180); cost (:130)
+  int32_t cost = 0;
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    inv[l] -= del[l];
+    bk[l] = fill[l] - del[l];
+    op[l] = inc[l] + act[l];
+    obs[l] = inv[l] - bk[l];
+    ic[l] = a.h * inv[l];
+    bc[l] = a.b * bk[l];
+    cost += ic[l] + bc[l];
+  }
+  if (a.hist) store_row<L>(a.hist + static_cast<int64_t>(wk.week) * stride + row, op);  // :123
+  return -cost;
+}
+
+template <int L>
+__device__ __forceinline__ void add_row(int32_t* __restrict__ p, const int32_t (&v)[L]) {
+  int32_t acc[L];
+  load_row<L>(p, acc);
+#pragma unroll
+  for (int l = 0; l < L; ++l) acc[l] += v[l];
+  store_row<L>(p, acc);
+}
+
+// step(action) for one env per lane: state in from HBM, one week, state out.
+template <int L>
+__global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const WeekInfo wk) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= a.n) return;
+  const int64_t row = n * L;
+  int32_t inv[L], bk[L], op[L], act[L], obs[L], ic[L], bc[L];
+  load_row<L>(a.inv + row, inv);
+  load_row<L>(a.bk + row, bk);
+  load_row<L>(a.op + row, op);
+  load_row<L>(a.act + row, act);
+  const int32_t reward = step_core<L>(a, n, wk, a.episode, inv, bk, op, act, obs, ic, bc);
+  a.rew[n] = reward;
+  const bool terminal = wk.flags & 1;
+  if (terminal && a.term_obs) store_row<L>(a.term_obs + row, obs);
+  if (a.ep_ret) {
+    const int64_t r = a.ep_ret[n] + reward;
+    if (terminal && a.final_ret) a.final_ret[n] = r;
+    a.ep_ret[n] = r;
+  }
+  if (wk.flags & 2) {  // auto-reset: the next step starts a fresh episode
+    reset_env<L>(a, n, a.obs);
+    return;
+  }
+  store_row<L>(a.inv + row, inv);
+  store_row<L>(a.bk + row, bk);
+  store_row<L>(a.op + row, op);
+  store_row<L>(a.obs + row, obs);
+  if (a.inv_acc) add_row<L>(a.inv_acc + row, ic);  // :131
+  if (a.bk_acc) add_row<L>(a.bk_acc + row, bc);    // :132
+}
+
+// K weeks per launch, inventory/backlog/orders/ledgers/return in registers; only the
+// pipeline ring (RMW through L2), actions in and obs/rewards out touch memory per week.
+struct RolloutWeeks {
+  WeekInfo wk[SCG_BG_ROLLOUT_MAX];
+};
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int32_t K, const RolloutWeeks weeks,
+                                                            const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
+                                                            int32_t* __restrict__ rew_out) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= a.n) return;
+  const int64_t row = n * L;
+  const int64_t stride = a.n * L;
+  int32_t inv[L], bk[L], op[L], iacc[L], bacc[L];
+  load_row<L>(a.inv + row, inv);
+  load_row<L>(a.bk + row, bk);
+  load_row<L>(a.op + row, op);
+#pragma unroll
+  for (int l = 0; l < L; ++l) iacc[l] = bacc[l] = 0;
+  if (a.inv_acc) load_row<L>(a.inv_acc + row, iacc);
+  if (a.bk_acc) load_row<L>(a.bk_acc + row, bacc);
+  int64_t ret = a.ep_ret ? a.ep_ret[n] : 0;
+  uint32_t episode = a.episode;
+  for (int32_t k = 0; k < K; ++k) {
+    const WeekInfo wk = weeks.wk[k];
+    int32_t act[L], obs[L], ic[L], bc[L];
+    load_row<L>(acts + k * stride + row, act);
+    const int32_t reward = step_core<L>(a, n, wk, episode, inv, bk, op, act, obs, ic, bc);
+    ret += reward;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      iacc[l] += ic[l];
+      bacc[l] += bc[l];
+    }
+    if ((wk.flags & 1) && a.final_ret) a.final_ret[n] = ret;
+    if (wk.flags & 2) {  // auto-reset in registers (:140-156)
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        inv[l] = a.init_inv[l];
+        bk[l] = 0;
+        op[l] = a.orders_value;
+        iacc[l] = bacc[l] = 0;
+        obs[l] = inv[l];
+      }
+      for (int t = 1; t <= a.init_slots; ++t) fill_row<L>(a.ring + (t % a.ring_slots) * stride + row, a.ship_value);
+      if (a.hist) fill_row<L>(a.hist + row, a.orders_value);
+      ret = 0;
+      ++episode;
+    }
+    if (obs_out) store_row<L>(obs_out + k * stride + row, obs);
+    if (rew_out) rew_out[k * a.n + n] = reward;
+  }
+  store_row<L>(a.inv + row, inv);
+  store_row<L>(a.bk + row, bk);
+  store_row<L>(a.op + row, op);
+  if (a.inv_acc) store_row<L>(a.inv_acc + row, iacc);
+  if (a.bk_acc) store_row<L>(a.bk_acc + row, bacc);
+  if (a.ep_ret) a.ep_ret[n] = ret;
+}
+
+// Philox draws for tests/benchmarks ------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void poisson_demand_kernel(const BgArgs a, int32_t weeks,
+                                                                int32_t* __restrict__ out) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= a.n) return;
+  for (int32_t w = 1; w <= weeks; ++w) out[(int64_t)(w - 1) * a.n + n] = week_demand(a, n, w, a.episode);
+}
+
+__global__ __launch_bounds__(kBlock) void uniform_ints_kernel(uint32_t k0, uint32_t k1, int64_t env_offset,
+                                                              int64_t n_envs, int32_t rows, int32_t width,
+                                                              uint32_t tag, int32_t lo, uint32_t range,
+                                                              int32_t* __restrict__ out) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= n_envs) return;
+  const uint32_t env = static_cast<uint32_t>(env_offset + n);
+  const int32_t words = rows * width;
+  for (int32_t j0 = 0; j0 < words; j0 += 4) {
+    const scg::U4 r = scg::philox4x32_10(scg::U4{env, tag, static_cast<uint32_t>(j0 >> 2), SCG_STREAM_ACTION}, k0, k1);
+    const uint32_t w4[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int32_t j = j0 + s;
+      if (j < words) {
+        const uint32_t v = static_cast<uint32_t>((static_cast<uint64_t>(w4[s]) * range) >> 32);
+        const int32_t rrow = j / width, col = j - rrow * width;
+        out[((int64_t)rrow * n_envs + n) * width + col] = lo + static_cast<int32_t>(v);
+      }
+    }
+  }
+}
+
+// ---- host helpers ---------------------------------------------------------------------
+#define SCG_LEVEL_CASES(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+
+int launch_reset(int L, dim3 grid, hipStream_t s, const BgArgs& a) {
+  switch (L) {
+#define X(l) case l: hipLaunchKernelGGL(bg_reset_kernel<l>, grid, dim3(kBlock), 0, s, a); break;
+    SCG_LEVEL_CASES(X)
+#undef X
+    default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
+  }
+  return check_launch("bg_reset_kernel");
+}
+
+int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk) {
+  switch (L) {
+#define X(l) case l: hipLaunchKernelGGL(bg_step_kernel<l>, grid, dim3(kBlock), 0, s, a, wk); break;
+    SCG_LEVEL_CASES(X)
+#undef X
+    default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
+  }
+  return check_launch("bg_step_kernel");
+}
+
+int launch_rollout(int L, dim3 grid, hipStream_t s, const BgArgs& a, int32_t K, const RolloutWeeks& weeks,
+                   const int32_t* acts, int32_t* obs, int32_t* rew) {
+  switch (L) {
+#define X(l) case l: hipLaunchKernelGGL(bg_rollout_kernel<l>, grid, dim3(kBlock), 0, s, a, K, weeks, acts, obs, rew); break;
+    SCG_LEVEL_CASES(X)
+#undef X
+    default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
+  }
+  return check_launch("bg_rollout_kernel");
+}
+
+int check_state(const scg_bg_config* cfg, const scg_bg_state* st) {
+  if (!cfg || !st) return fail(SCG_ERR_INVALID, "null config/state");
+  if (!cfg->plan || cfg->ring_slots <= 0) return fail(SCG_ERR_INVALID, "config not prepared (call scg_bg_prepare)");
+  if (st->n_envs <= 0) return fail(SCG_ERR_INVALID, "n_envs must be > 0");
+  if (st->env_offset < 0 || st->env_offset + st->n_envs > (int64_t(1) << 32))
+    return fail(SCG_ERR_INVALID, "global env ids must fit in 32 bits");
+  if (!st->inventory || !st->backlog || !st->orders_placed || !st->shipments)
+    return fail(SCG_ERR_INVALID, "state buffers inventory/backlog/orders_placed/shipments are required");
+  if (cfg->demand_mode == SCG_DEMAND_TABLE && !cfg->demand_table)
+    return fail(SCG_ERR_INVALID, "TABLE demand mode needs demand_table");
+  if (cfg->demand_mode == SCG_DEMAND_POISSON && !cfg->poisson_thresholds)
+    return fail(SCG_ERR_INVALID, "POISSON demand mode needs poisson_thresholds");
+  return SCG_OK;
+}
+
+BgArgs make_args(const scg_bg_config* cfg, const scg_bg_state* st) {
+  BgArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.inv = st->inventory;
+  a.bk = st->backlog;
+  a.op = st->orders_placed;
+  a.ring = st->shipments;
+  a.inv_acc = st->inventory_costs;
+  a.bk_acc = st->backlog_costs;
+  a.hist = st->orders_history;
+  a.ep_ret = st->episode_return;
+  a.final_ret = st->final_return;
+  a.demand_table = cfg->demand_table;
+  a.pthr = cfg->poisson_thresholds;
+  a.n = st->n_envs;
+  a.env_offset = st->env_offset;
+  a.key0 = static_cast<uint32_t>(st->seed & 0xffffffffu);
+  a.key1 = static_cast<uint32_t>(st->seed >> 32);
+  a.episode = st->episode;
+  a.demand_mode = cfg->demand_mode;
+  a.pthr_len = cfg->poisson_len;
+  a.h = cfg->inv_cost;
+  a.b = cfg->backlog_cost;
+  a.ship_value = cfg->initial_shipment_value;
+  a.orders_value = cfg->initial_orders_value;
+  a.init_slots = std::min(cfg->shipment_delays ? cfg->shipment_delays[0] : 0, cfg->max_weeks);
+  a.ring_slots = cfg->ring_slots;
+  for (int l = 0; l < cfg->levels; ++l) a.init_inv[l] = cfg->initial_inventory[l];
+  return a;
+}
+
+inline dim3 grid_for(int64_t n) { return dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)); }
+
+}  // namespace scg
+
+using namespace scg;
+
+// ========================================================================================
+extern "C" {
+
+int scg_abi_version(void) { return SCG_ABI_VERSION; }
+
+const char* scg_last_error(void) { return g_err; }
+
+int scg_bg_struct_sizes(size_t* config_size, size_t* state_size) {
+  if (config_size) *config_size = sizeof(scg_bg_config);
+  if (state_size) *state_size = sizeof(scg_bg_state);
+  return SCG_OK;
+}
+
+int scg_poisson_table(double lam, uint32_t* out, int32_t cap) {
+  if (!(lam >= 0.0) || std::isinf(lam)) return -fail(SCG_ERR_INVALID, "poisson lambda must be finite and >= 0");
+  if (!out || cap <= 0) return -fail(SCG_ERR_INVALID, "null/empty threshold buffer");
+  double p = std::exp(-lam);
+  double c = p;
+  for (int32_t k = 0; k < cap; ++k) {
+    const double t = c * 4294967296.0;
+    const uint32_t v = t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t);
+    out[k] = v;
+    if (v == 0xffffffffu) return k + 1;
+    p = p * lam / static_cast<double>(k + 1);
+    c = c + p;
+  }
+  return -fail(SCG_ERR_INVALID, "poisson lambda %g needs more than %d thresholds", lam, cap);
+}
+
+int scg_bg_prepare(scg_bg_config* cfg) {
+  if (!cfg) return fail(SCG_ERR_INVALID, "null config");
+  const int32_t L = cfg->levels, T = cfg->max_weeks;
+  if (L < 1 || L > SCG_BG_MAX_LEVELS) return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
+  if (T < 1 || T > SCG_BG_MAX_WEEKS) return fail(SCG_ERR_INVALID, "max_weeks=%d outside 1..%d", T, SCG_BG_MAX_WEEKS);
+  if (!cfg->shipment_delays || !cfg->plan) return fail(SCG_ERR_INVALID, "shipment_delays and plan are required");
+  if (cfg->demand_mode < SCG_DEMAND_FIXED || cfg->demand_mode > SCG_DEMAND_POISSON)
+    return fail(SCG_ERR_INVALID, "unknown demand_mode %d", cfg->demand_mode);
+  if (cfg->demand_mode == SCG_DEMAND_FIXED && !cfg->customer_demand)
+    return fail(SCG_ERR_INVALID, "FIXED demand mode needs customer_demand");
+  if (cfg->demand_mode == SCG_DEMAND_POISSON && (cfg->poisson_len < 1 || cfg->poisson_len > SCG_POISSON_MAX))
+    return fail(SCG_ERR_INVALID, "poisson_len=%d outside 1..%d", cfg->poisson_len, SCG_POISSON_MAX);
+  int32_t max_delay = 0;
+  for (int32_t w = 0; w <= T; ++w) {
+    const int32_t d = cfg->shipment_delays[w];
+    if (d < 0 || d > SCG_BG_MAX_DELAY)
+      return fail(SCG_ERR_INVALID, "shipment_delays[%d]=%d outside 0..%d", w, d, SCG_BG_MAX_DELAY);
+    max_delay = std::max(max_delay, d);
+  }
+  const int32_t R = max_delay + 1;
+  // Which arrival weeks have been written, in week order (writes only target later weeks).
+  std::vector<uint8_t> written(static_cast<size_t>(T) + 2, 0);
+  const int32_t d0 = cfg->shipment_delays[0];
+  for (int32_t t = 1; t <= std::min(d0, T); ++t) written[t] = 1;  // initial pipeline (:52)
+  cfg->plan[0] = 0;
+  for (int32_t w = 1; w <= T; ++w) {
+    const int32_t d = cfg->shipment_delays[w];
+    int32_t mode;
+    if (d == 0) {
+      mode = MODE_DIRECT;                 // :93-94, :111-112
+    } else if (w + d > T) {
+      mode = MODE_DROP;                   // lands after the last step: never received
+    } else if (written[w + d]) {
+      mode = MODE_ADD;                    // several weeks ship into one arrival week
+    } else {
+      mode = MODE_STORE;
+      written[w + d] = 1;
+    }
+    cfg->plan[w] = mode | (written[w] ? PLAN_ARRIVE : 0) | (d << 8);
+  }
+  cfg->ring_slots = R;
+  return SCG_OK;
+}
+
+int scg_bg_reset(const scg_bg_config* cfg, scg_bg_state* st, int32_t* obs, void* stream) {
+  if (int rc = check_state(cfg, st)) return rc;
+  if (st->week >= 0) st->episode += 1;  // the previous episode (finished or not) is discarded
+  BgArgs a = make_args(cfg, st);
+  a.obs = obs;
+  if (int rc = launch_reset(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a)) return rc;
+  st->week = 0;
+  return SCG_OK;
+}
+
+// Per-week launch info for week w of the current episode.
+static scg::WeekInfo week_info(const scg_bg_config* cfg, int32_t w, uint32_t flags) {
+  const int32_t p = cfg->plan[w];
+  const int32_t R = cfg->ring_slots;
+  WeekInfo wk;
+  wk.week = w;
+  wk.read_slot = plan_arrive(p) ? w % R : -1;
+  wk.write_slot = (w + plan_delay(p)) % R;
+  wk.mode = plan_mode(p);
+  wk.demand_fixed = cfg->demand_mode == SCG_DEMAND_FIXED ? cfg->customer_demand[w - 1] : 0;
+  const bool terminal = (w == cfg->max_weeks);
+  wk.flags = (terminal ? 1 : 0) | ((terminal && (flags & SCG_BG_AUTORESET)) ? 2 : 0);
+  return wk;
+}
+
+static int check_step(const scg_bg_config* cfg, const scg_bg_state* st) {
+  if (st->week < 0) return fail(SCG_ERR_NOT_RESET, "step() before reset()");
+  if (st->week >= cfg->max_weeks)
+    return fail(SCG_ERR_PAST_HORIZON, "step() after the terminal week %d (customer_demand has %d weeks)",
+                cfg->max_weeks, cfg->max_weeks);
+  return SCG_OK;
+}
+
+int scg_bg_step(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* action, int32_t* obs,
+                int32_t* reward, int32_t* terminal_obs, uint32_t flags, int32_t* done, void* stream) {
+  if (int rc = check_state(cfg, st)) return rc;
+  if (!action || !obs || !reward) return fail(SCG_ERR_INVALID, "action/obs/reward buffers are required");
+  if (int rc = check_step(cfg, st)) return rc;
+  const int32_t w = st->week + 1;
+  const WeekInfo wk = week_info(cfg, w, flags);
+  BgArgs a = make_args(cfg, st);
+  a.act = action;
+  a.obs = obs;
+  a.rew = reward;
+  a.term_obs = terminal_obs;
+  if (int rc = launch_step(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a, wk)) return rc;
+  if (wk.flags & 2) {
+    st->week = 0;
+    st->episode += 1;
+  } else {
+    st->week = w;
+  }
+  if (done) *done = (wk.flags & 1) ? 1 : 0;
+  return SCG_OK;
+}
+
+int scg_bg_rollout(const scg_bg_config* cfg, scg_bg_state* st, int32_t n_weeks, const int32_t* actions,
+                   int32_t* obs, int32_t* rewards, uint32_t flags, void* stream) {
+  if (int rc = check_state(cfg, st)) return rc;
+  if (!actions || n_weeks < 0) return fail(SCG_ERR_INVALID, "rollout needs actions and n_weeks >= 0");
+  if (int rc = check_step(cfg, st)) return rc;
+  if (!(flags & SCG_BG_AUTORESET) && st->week + static_cast<int64_t>(n_weeks) > cfg->max_weeks)
+    return fail(SCG_ERR_PAST_HORIZON, "rollout of %d weeks from week %d passes the terminal week %d", n_weeks,
+                st->week, cfg->max_weeks);
+  const int64_t stride = st->n_envs * cfg->levels;
+  int32_t done_k = 0;
+  while (done_k < n_weeks) {
+    // one launch covers up to SCG_BG_ROLLOUT_MAX weeks; without auto-reset it stops at T
+    RolloutWeeks weeks;
+    int32_t K = 0;
+    scg_bg_state probe = *st;
+    BgArgs a = make_args(cfg, st);
+    while (K < SCG_BG_ROLLOUT_MAX && done_k + K < n_weeks) {
+      const int32_t w = probe.week + 1;
+      weeks.wk[K] = week_info(cfg, w, flags);
+      if (weeks.wk[K].flags & 2) {
+        probe.week = 0;
+        probe.episode += 1;
+      } else {
+        probe.week = w;
+      }
+      ++K;
+    }
+    if (int rc = launch_rollout(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a, K, weeks,
+                                actions + done_k * stride, obs ? obs + done_k * stride : nullptr,
+                                rewards ? rewards + done_k * st->n_envs : nullptr))
+      return rc;
+    st->week = probe.week;
+    st->episode = probe.episode;
+    done_k += K;
+  }
+  return SCG_OK;
+}
+
+int scg_bg_poisson_demand(const scg_bg_config* cfg, const scg_bg_state* st, uint32_t episode, int32_t* out,
+                          void* stream) {
+  if (int rc = check_state(cfg, st)) return rc;
+  if (!out) return fail(SCG_ERR_INVALID, "null output");
+  if (cfg->demand_mode != SCG_DEMAND_POISSON) return fail(SCG_ERR_INVALID, "config is not in POISSON demand mode");
+  BgArgs a = make_args(cfg, st);
+  a.episode = episode;
+  hipLaunchKernelGGL(poisson_demand_kernel, grid_for(st->n_envs), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     a, cfg->max_weeks, out);
+  return check_launch("poisson_demand_kernel");
+}
+
+int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, int32_t rows, int32_t width, uint32_t tag,
+                     int32_t lo, int32_t hi, int32_t* out, void* stream) {
+  if (!out || n_envs <= 0 || rows <= 0 || width <= 0 || hi < lo)
+    return fail(SCG_ERR_INVALID, "bad uniform_ints arguments");
+  const uint32_t range = static_cast<uint32_t>(static_cast<int64_t>(hi) - lo + 1);  // 0 means 2^32
+  if (range == 0) return fail(SCG_ERR_INVALID, "uniform_ints range must be < 2^32");
+  hipLaunchKernelGGL(uniform_ints_kernel, grid_for(n_envs), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     static_cast<uint32_t>(seed & 0xffffffffu), static_cast<uint32_t>(seed >> 32), env_offset, n_envs,
+                     rows, width, tag, lo, range, out);
+  return check_launch("uniform_ints_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+"""gym_supplychain_amd — MI355X-native vectorised environments of caburu/gym-supplychain.
+
+Drop-in for the reference's hot path: the gym ids it registers (gym_supplychain/
+__init__.py:1-51) map to classes with the reference's names and gym API, whose step()
+dynamics run as fused HIP kernels through the C ABI in include/scgpu.h.
+
+    import gym_supplychain_amd as gsa
+    env = gsa.make("beergame-v0")                       # one env, reference API
+    venv = gsa.make_vec("beergame-v0", 65536, demand="poisson", seed=0)   # batched
+"""
+from . import _native  # noqa: F401  (fails loudly when libscgpu.so is missing)
+from .envs import BeerGameEnv, BeerGameVecEnv
+
+__all__ = ["BeerGameEnv", "BeerGameVecEnv", "ENV_IDS", "VEC_ENV_IDS", "make", "make_vec", "register_gym"]
+
+# id -> entry point, as registered by the reference (gym_supplychain/__init__.py:3-6)
+ENV_IDS = {
+    "beergame-v0": "gym_supplychain_amd.envs:BeerGameEnv",
+}
+VEC_ENV_IDS = {
+    "beergame-v0": BeerGameVecEnv,
+}
+
+
+def _resolve(entry_point):
+    mod, _, name = entry_point.partition(":")
+    import importlib
+    return getattr(importlib.import_module(mod), name)
+
+
+def make(id, **kwargs):
+    """Construct the single-env class registered under `id` (gym.make equivalent)."""
+    if id not in ENV_IDS:
+        raise KeyError(f"unknown env id {id!r}; available: {sorted(ENV_IDS)}")
+    return _resolve(ENV_IDS[id])(**kwargs)
+
+
+def make_vec(id, n_envs, **kwargs):
+    """Construct the batched (N envs per GPU) class for `id`."""
+    if id not in VEC_ENV_IDS:
+        raise KeyError(f"no vectorised env for {id!r}; available: {sorted(VEC_ENV_IDS)}")
+    return VEC_ENV_IDS[id](n_envs, **kwargs)
+
+
+def register_gym():
+    """Register the ids with gym/gymnasium when one is installed (no-op otherwise)."""
+    for modname in ("gymnasium", "gym"):
+        try:
+            reg = __import__(modname + ".envs.registration", fromlist=["register"])
+        except ImportError:
+            continue
+        for env_id, ep in ENV_IDS.items():
+            try:
+                reg.register(id=env_id, entry_point=ep)
+            except Exception:  # already registered
+                pass
+        return True
+    return False

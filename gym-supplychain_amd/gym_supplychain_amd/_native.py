@@ -1,0 +1,169 @@
+"""ctypes binding of libscgpu.so, the C ABI declared in include/scgpu.h.
+
+The library is built in-tree (``__graft_entry__.build()`` / ``python -m
+gym_supplychain_amd.build``) next to this file. There is no CPU fallback: every env
+in this package runs its dynamics through these entry points, and importing this
+module raises when the library is missing or was built for another ABI.
+
+torch is imported first on purpose: torch ships its own libamdhip64.so (soname
+libamdhip64.so.7) and the dynamic loader then binds libscgpu.so to that same HIP
+runtime, so torch's streams and allocations are valid handles for our kernels.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime libscgpu.so binds to)
+
+LIB_NAME = "libscgpu.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+ABI_VERSION = 1
+
+SCG_OK = 0
+SCG_ERR_INVALID = 1
+SCG_ERR_PAST_HORIZON = 2
+SCG_ERR_NOT_RESET = 3
+SCG_ERR_HIP = 4
+
+SCG_DEMAND_FIXED = 0
+SCG_DEMAND_TABLE = 1
+SCG_DEMAND_POISSON = 2
+
+SCG_BG_AUTORESET = 1
+SCG_STREAM_DEMAND = 0
+SCG_STREAM_ACTION = 1
+
+BG_MAX_LEVELS = 16
+BG_MAX_WEEKS = 4096
+BG_MAX_DELAY = 63
+POISSON_MAX = 256
+BG_ROLLOUT_MAX = 128
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+class BgConfig(ctypes.Structure):
+    """scg_bg_config (include/scgpu.h)."""
+    _fields_ = [
+        ("levels", ctypes.c_int32),
+        ("max_weeks", ctypes.c_int32),
+        ("inv_cost", ctypes.c_int32),
+        ("backlog_cost", ctypes.c_int32),
+        ("initial_shipment_value", ctypes.c_int32),
+        ("initial_orders_value", ctypes.c_int32),
+        ("initial_inventory", ctypes.c_int32 * BG_MAX_LEVELS),
+        ("demand_mode", ctypes.c_int32),
+        ("poisson_len", ctypes.c_int32),
+        ("shipment_delays", ctypes.c_void_p),
+        ("customer_demand", ctypes.c_void_p),
+        ("demand_table", ctypes.c_void_p),
+        ("poisson_thresholds", ctypes.c_void_p),
+        ("plan", ctypes.c_void_p),
+        ("ring_slots", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class BgState(ctypes.Structure):
+    """scg_bg_state (include/scgpu.h)."""
+    _fields_ = [
+        ("n_envs", ctypes.c_int64),
+        ("env_offset", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("episode", ctypes.c_uint32),
+        ("week", ctypes.c_int32),
+        ("inventory", ctypes.c_void_p),
+        ("backlog", ctypes.c_void_p),
+        ("orders_placed", ctypes.c_void_p),
+        ("shipments", ctypes.c_void_p),
+        ("inventory_costs", ctypes.c_void_p),
+        ("backlog_costs", ctypes.c_void_p),
+        ("orders_history", ctypes.c_void_p),
+        ("episode_return", ctypes.c_void_p),
+        ("final_return", ctypes.c_void_p),
+    ]
+
+
+# Every symbol include/scgpu.h declares, with its ctypes signature.
+SIGNATURES = {
+    "scg_abi_version": (ctypes.c_int, []),
+    "scg_last_error": (ctypes.c_char_p, []),
+    "scg_bg_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
+    "scg_poisson_table": (ctypes.c_int, [ctypes.c_double, _u32p, ctypes.c_int32]),
+    "scg_bg_prepare": (ctypes.c_int, [ctypes.POINTER(BgConfig)]),
+    "scg_bg_reset": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
+                                    ctypes.c_void_p]),
+    "scg_bg_step": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                   _i32p, ctypes.c_void_p]),
+    "scg_bg_rollout": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                      ctypes.c_void_p]),
+    "scg_bg_poisson_demand": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState),
+                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "scg_uniform_ints": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+
+class NativeLibraryError(ImportError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(gym_supplychain_amd has no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.scg_abi_version() != ABI_VERSION:
+        raise NativeLibraryError(f"{LIB_PATH} ABI {lib.scg_abi_version()} != expected {ABI_VERSION}; rebuild it")
+    cs, ss = ctypes.c_size_t(), ctypes.c_size_t()
+    lib.scg_bg_struct_sizes(ctypes.byref(cs), ctypes.byref(ss))
+    if (cs.value, ss.value) != (ctypes.sizeof(BgConfig), ctypes.sizeof(BgState)):
+        raise NativeLibraryError(f"struct layout mismatch: C ({cs.value}, {ss.value}) vs ctypes "
+                                 f"({ctypes.sizeof(BgConfig)}, {ctypes.sizeof(BgState)})")
+    return lib
+
+
+lib = _load()
+
+
+def last_error():
+    msg = lib.scg_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc):
+    """Map an scg_status to the exception the reference raises for the same misuse."""
+    if rc == SCG_OK:
+        return
+    msg = last_error()
+    if rc == SCG_ERR_INVALID:
+        raise ValueError(msg)
+    if rc == SCG_ERR_PAST_HORIZON:
+        raise IndexError(msg)
+    raise RuntimeError(msg or f"scgpu error {rc}")
+
+
+def poisson_table(lam):
+    """uint32 CDF thresholds for Poisson(lam), as a Python list (scg_poisson_table)."""
+    buf = (ctypes.c_uint32 * POISSON_MAX)()
+    n = lib.scg_poisson_table(float(lam), buf, POISSON_MAX)
+    if n < 0:
+        check(-n)
+    return list(buf[:n])
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)

@@ -1,0 +1,64 @@
+"""Multi-GPU sharding for the vectorised envs: one process per GPU, envs never interact.
+
+Rank r owns global env ids [r * n_per_rank, (r + 1) * n_per_rank). Every per-env draw
+(Philox counter = global env id, episode, week) depends only on the global id, so a
+trajectory is identical at 1, 2, 4 or 8 GPUs (tests/test_gpu_beergame.py
+test_sharding_is_invariant). The data path has no collective; the only exchange is the
+end-of-episode metric gather, an RCCL all-gather over xGMI issued asynchronously so it
+overlaps the next episode's steps (the north star's "all-gather for the end-of-episode
+reward/metric reduction").
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def rank_world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def shard_offset(n_per_rank, rank=None):
+    """Global id of this rank's first env."""
+    if rank is None:
+        rank = rank_world()[0]
+    return int(rank) * int(n_per_rank)
+
+
+class EpisodeReturnGather:
+    """All-gather of every env's finished-episode return, overlapped with compute.
+
+    on_episode_end(final_return) snapshots the per-env int64 returns on the producing
+    stream (so the next episode may overwrite the env's buffer) and launches an async
+    all-gather; result() waits for the latest one and returns the global [world * N]
+    tensor. With one process it degenerates to the snapshot.
+    """
+
+    def __init__(self, n_per_rank, device, group=None):
+        self.rank, self.world = rank_world()
+        self.group = group
+        self.n = int(n_per_rank)
+        self.device = torch.device(device)
+        self._stage = torch.zeros(self.n, dtype=torch.int64, device=self.device)
+        self._out = torch.zeros(self.world * self.n, dtype=torch.int64, device=self.device)
+        self._work = None
+        self.gathers = 0
+
+    def on_episode_end(self, final_return):
+        if self._work is not None:
+            self._work.wait()  # previous gather still reading _stage
+        self._stage.copy_(final_return, non_blocking=True)
+        if self.world > 1:
+            self._work = dist.all_gather_into_tensor(self._out, self._stage, group=self.group, async_op=True)
+        else:
+            self._out.copy_(self._stage, non_blocking=True)
+            self._work = None
+        self.gathers += 1
+
+    def result(self):
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        return self._out

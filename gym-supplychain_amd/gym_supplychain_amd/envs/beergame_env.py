@@ -1,0 +1,434 @@
+"""MIT Beer Game on MI355X: batched ``BeerGameVecEnv`` and the drop-in ``BeerGameEnv``.
+
+Mirrors gym_supplychain.envs.BeerGameEnv (gym_supplychain/envs/beergame_env.py,
+reference snapshot 2024-08-07): same env_init_info keys and defaults (:16-43), same
+reset()/step() results (:66-156), same exceptions for the same misuse. The dynamics run
+in HIP kernels (gym-supplychain_amd/csrc/scg_beergame.hip) through the C ABI of
+include/scgpu.h; this module only owns device buffers and marshals arguments.
+
+Differences from the reference, all documented in DESIGN.md:
+  * state is int32 (the reference's int64 values are reproduced exactly while they fit);
+  * actions are integers — a float action is truncated toward zero on input;
+  * BeerGameVecEnv adds per-env demand (a device table, or Poisson draws made on device
+    with Philox4x32-10) and auto-reset; the reference has one fixed demand list (F2).
+"""
+import ctypes
+import numbers
+
+import numpy as np
+import torch
+
+from .. import _native as nat
+from .. import spaces
+
+# beergame_env.py:16-23
+STD_LEVELS = 4
+STD_DEMAND = [4] * 4 + [8] * 31
+STD_INVENTORY = 12
+STD_SHIP_DELAY = 2
+STD_SHIP_VALUE = 4
+STD_ORDERS_VALUE = 4
+STD_INV_COST = 1
+STD_BACKLOG_COST = 2
+
+_I32 = (-(2 ** 31), 2 ** 31 - 1)
+
+
+def _int32(name, v):
+    if isinstance(v, (bool, np.bool_)) or not isinstance(v, (numbers.Integral, np.integer)):
+        # the reference's ledgers are int arrays: a float cost fails at its first step (:131)
+        raise TypeError(f"{name} must be an integer, got {type(v).__name__}")
+    v = int(v)
+    if not _I32[0] <= v <= _I32[1]:
+        raise ValueError(f"{name}={v} does not fit int32")
+    return v
+
+
+def _int32_list(name, seq):
+    arr = np.asarray(seq)
+    if arr.dtype.kind == "f":
+        arr = arr.astype(np.int64)  # np.asarray(..., dtype=int) truncation (:33, :35)
+    arr = arr.astype(np.int64).reshape(-1)
+    if arr.size and (arr.min() < _I32[0] or arr.max() > _I32[1]):
+        raise ValueError(f"{name} does not fit int32")
+    return arr.astype(np.int32)
+
+
+class BeerGameConfig:
+    """env_init_info resolved as BeerGameEnv.__init__ does (beergame_env.py:11-58)."""
+
+    def __init__(self, env_init_info=None, horizon=None):
+        info = dict(env_init_info or {})
+        self.levels = _int32("levels", info.get("levels", STD_LEVELS))
+        if not 1 <= self.levels <= nat.BG_MAX_LEVELS:
+            raise ValueError(f"levels={self.levels} outside 1..{nat.BG_MAX_LEVELS}")
+        self.inv_cost = _int32("inv_cost", info.get("inv_cost", STD_INV_COST))
+        self.backlog_cost = _int32("backlog_cost", info.get("backlog_cost", STD_BACKLOG_COST))
+        self.customer_demand = _int32_list("customer_demand", info.get("customer_demand", STD_DEMAND))
+        # T = len(customer_demand) (:37); a per-env demand source may set its own horizon
+        self.max_weeks = int(horizon) if horizon is not None else int(self.customer_demand.size)
+        if not 1 <= self.max_weeks <= nat.BG_MAX_WEEKS:
+            raise ValueError(f"episode length {self.max_weeks} outside 1..{nat.BG_MAX_WEEKS}")
+        inv0 = info.get("initial_inventory", STD_INVENTORY + np.zeros(STD_LEVELS))
+        self.initial_inventory = _int32_list("initial_inventory", inv0)
+        if self.initial_inventory.size != self.levels:
+            # the reference fails later with a broadcast error; fail at construction
+            raise ValueError(f"initial_inventory has {self.initial_inventory.size} entries, levels={self.levels}")
+        # :39 — index 0 is the initial pipeline delay, always 2, then one delay per week
+        user_delays = info.get("shipment_delays", [STD_SHIP_DELAY] * self.max_weeks)
+        if isinstance(user_delays, np.ndarray):
+            user_delays = user_delays.tolist()
+        self.shipment_delays = _int32_list("shipment_delays", [STD_SHIP_DELAY] + list(user_delays))
+        if self.shipment_delays.size < self.max_weeks + 1:
+            # the reference's table sizing reads shipment_delays[0..T] (:47-48)
+            raise IndexError(f"shipment_delays needs {self.max_weeks} entries, got {self.shipment_delays.size - 1}")
+        self.shipment_delays = self.shipment_delays[: self.max_weeks + 1].copy()
+        if self.shipment_delays.min() < 0 or self.shipment_delays.max() > nat.BG_MAX_DELAY:
+            raise ValueError(f"shipment delays must be within 0..{nat.BG_MAX_DELAY}")
+        self.initial_shipment_value = _int32("initial_shipment_value",
+                                             info.get("initial_shipment_value", STD_SHIP_VALUE))
+        self.initial_orders_value = _int32("initial_orders_value", info.get("initial_orders_value", STD_ORDERS_VALUE))
+
+
+class BeerGameVecEnv:
+    """N lock-step Beer Game envs on one GPU, state resident in HBM.
+
+    reset() -> obs int32 [N, L]
+    step(actions int32 [N, L]) -> (obs [N, L], reward int32 [N], done bool [N], info)
+
+    Returned tensors are views of this env's output buffers, overwritten by the next
+    call (clone() to keep them). With auto_reset (default) the step that reaches the
+    terminal week resets every env in the same kernel: obs is then the reset
+    observation and info holds 'terminal_observation' and 'episode_return'.
+
+    demand: "fixed" — env_init_info['customer_demand'] for every env (reference);
+            "poisson" — Poisson(poisson_lambda) per (env, episode, week), Philox4x32-10
+                        keyed by `seed`, counter (env_offset + n, episode, week, 0);
+            a device tensor int32 [T, N] — caller-supplied per-env demand.
+    env_offset: global id of env 0 — shards on several GPUs draw the same per-env
+            demand as one big batch would (multi-GPU invariant).
+    """
+
+    def __init__(self, n_envs, env_init_info=None, demand="fixed", poisson_lambda=8.0, seed=0, device=None,
+                 env_offset=0, auto_reset=True, track_costs=True, track_history=False, track_returns=True,
+                 horizon=None):
+        n_envs = int(n_envs)
+        if n_envs < 1:
+            raise ValueError("n_envs must be >= 1")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise ValueError("BeerGameVecEnv runs on a GPU device (no CPU fallback)")
+        table = None
+        if isinstance(demand, torch.Tensor):
+            table = demand
+            horizon = table.shape[0]
+            mode = nat.SCG_DEMAND_TABLE
+        elif demand == "fixed":
+            mode = nat.SCG_DEMAND_FIXED
+        elif demand == "poisson":
+            mode = nat.SCG_DEMAND_POISSON
+        else:
+            raise ValueError(f"demand must be 'fixed', 'poisson' or a device tensor, got {demand!r}")
+        cfg = BeerGameConfig(env_init_info, horizon=horizon)
+        if mode == nat.SCG_DEMAND_FIXED and cfg.customer_demand.size < cfg.max_weeks:
+            raise ValueError("customer_demand shorter than the horizon")
+        self.config = cfg
+        self.n_envs = n_envs
+        self.levels = L = cfg.levels
+        self.max_weeks = T = cfg.max_weeks
+        self.auto_reset = bool(auto_reset)
+        self.demand_mode = mode
+
+        # host-side arrays the C ABI reads (kept alive on self)
+        self._delays = (ctypes.c_int32 * (T + 1))(*cfg.shipment_delays.tolist())
+        self._demand = (ctypes.c_int32 * max(T, 1))(*cfg.customer_demand[:T].tolist()) \
+            if mode == nat.SCG_DEMAND_FIXED else None
+        self._plan = (ctypes.c_int32 * (T + 1))()
+
+        c = nat.BgConfig()
+        c.levels, c.max_weeks = L, T
+        c.inv_cost, c.backlog_cost = cfg.inv_cost, cfg.backlog_cost
+        c.initial_shipment_value = cfg.initial_shipment_value
+        c.initial_orders_value = cfg.initial_orders_value
+        for i, v in enumerate(cfg.initial_inventory.tolist()):
+            c.initial_inventory[i] = v
+        c.demand_mode = mode
+        c.shipment_delays = ctypes.cast(self._delays, ctypes.c_void_p)
+        c.customer_demand = ctypes.cast(self._demand, ctypes.c_void_p) if self._demand is not None else None
+        c.plan = ctypes.cast(self._plan, ctypes.c_void_p)
+        dev = self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        if mode == nat.SCG_DEMAND_TABLE:
+            if table.device != dev or table.dtype != torch.int32 or tuple(table.shape) != (T, n_envs):
+                raise ValueError(f"demand table must be int32 [{T}, {n_envs}] on {dev}")
+            self._table = table.contiguous()
+            c.demand_table = self._table.data_ptr()
+        if mode == nat.SCG_DEMAND_POISSON:
+            thr = nat.poisson_table(poisson_lambda)
+            self.poisson_lambda = float(poisson_lambda)
+            self._thresholds = torch.tensor(np.asarray(thr, dtype=np.uint32).view(np.int32), **i32)
+            c.poisson_thresholds = self._thresholds.data_ptr()
+            c.poisson_len = len(thr)
+        nat.check(nat.lib.scg_bg_prepare(ctypes.byref(c)))
+        self._cfg = c
+        self.ring_slots = R = c.ring_slots
+
+        # device state, env-major [N][L] int32 (DESIGN.md "Layout in HBM")
+        self._inv = torch.zeros((n_envs, L), **i32)
+        self._bk = torch.zeros((n_envs, L), **i32)
+        self._op = torch.zeros((n_envs, L), **i32)
+        self._ring = torch.zeros((R, n_envs, L), **i32)
+        self._inv_costs = torch.zeros((n_envs, L), **i32) if track_costs else None
+        self._bk_costs = torch.zeros((n_envs, L), **i32) if track_costs else None
+        self._hist = torch.zeros((T + 1, n_envs, L), **i32) if track_history else None
+        self._ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
+        self._final_ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
+        # outputs: obs and reward share one allocation so N=1 callers copy back once
+        self._out = torch.zeros(n_envs * L + n_envs, **i32)
+        self._obs = self._out[: n_envs * L].view(n_envs, L)
+        self._rew = self._out[n_envs * L:]
+        self._term_obs = torch.zeros((n_envs, L), **i32)
+        self._done_false = torch.zeros(n_envs, dtype=torch.bool, device=dev)
+        self._done_true = torch.ones(n_envs, dtype=torch.bool, device=dev)
+
+        s = nat.BgState()
+        s.n_envs, s.env_offset, s.seed = n_envs, int(env_offset), int(seed) & 0xFFFFFFFFFFFFFFFF
+        s.episode, s.week = 0, -1
+        s.inventory, s.backlog, s.orders_placed = self._inv.data_ptr(), self._bk.data_ptr(), self._op.data_ptr()
+        s.shipments = self._ring.data_ptr()
+        s.inventory_costs = self._inv_costs.data_ptr() if track_costs else None
+        s.backlog_costs = self._bk_costs.data_ptr() if track_costs else None
+        s.orders_history = self._hist.data_ptr() if track_history else None
+        s.episode_return = self._ret.data_ptr() if track_returns else None
+        s.final_return = self._final_ret.data_ptr() if track_returns else None
+        self._st = s
+        self._cfg_ref = ctypes.byref(self._cfg)
+        self._st_ref = ctypes.byref(self._st)
+        self._done_flag = ctypes.c_int32(0)
+        self._flags = nat.SCG_BG_AUTORESET if self.auto_reset else 0
+        # gym surface (an extension: the reference leaves both spaces unset, :62-64)
+        self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
+        self.single_action_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
+        self.observation_space = spaces.Box(_I32[0], _I32[1], (n_envs, L), np.int32)
+        self.action_space = spaces.Box(_I32[0], _I32[1], (n_envs, L), np.int32)
+
+    # -------------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self):
+        nat.check(nat.lib.scg_bg_reset(self._cfg_ref, self._st_ref, self._obs.data_ptr(), self._stream()))
+        return self._obs
+
+    def _actions(self, actions):
+        N, L = self.n_envs, self.levels
+        if not isinstance(actions, torch.Tensor):
+            actions = torch.as_tensor(np.asarray(actions))
+        if actions.dtype.is_floating_point:
+            actions = actions.trunc()
+        if actions.dtype != torch.int32 or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=torch.int32)
+        if actions.shape != (N, L):
+            if actions.numel() != N * L:
+                raise ValueError(f"actions must have shape ({N}, {L}), got {tuple(actions.shape)}")
+            actions = actions.reshape(N, L)
+        return actions.contiguous()
+
+    def step(self, actions):
+        act = self._actions(actions)
+        rc = nat.lib.scg_bg_step(self._cfg_ref, self._st_ref, act.data_ptr(), self._obs.data_ptr(),
+                                 self._rew.data_ptr(), self._term_obs.data_ptr(), self._flags,
+                                 ctypes.byref(self._done_flag), self._stream())
+        if rc:
+            nat.check(rc)
+        if self._done_flag.value:
+            info = {"terminal_observation": self._term_obs}
+            if self._final_ret is not None:
+                info["episode_return"] = self._final_ret
+            return self._obs, self._rew, self._done_true, info
+        return self._obs, self._rew, self._done_false, {}
+
+    def rollout(self, actions, obs_out=None, rewards_out=None):
+        """K weeks in as few launches as possible (state kept in registers).
+
+        actions int32 [K, N, L] on device. Returns (obs [K, N, L], rewards [K, N]); with
+        auto-reset the obs row of a terminal week is the reset observation, as in step().
+        """
+        if not isinstance(actions, torch.Tensor) or actions.device != self.device or actions.dtype != torch.int32:
+            actions = torch.as_tensor(actions).to(device=self.device, dtype=torch.int32)
+        actions = actions.contiguous()
+        K = actions.shape[0]
+        if tuple(actions.shape) != (K, self.n_envs, self.levels):
+            raise ValueError(f"actions must be [K, {self.n_envs}, {self.levels}]")
+        if obs_out is None:
+            obs_out = torch.empty((K, self.n_envs, self.levels), dtype=torch.int32, device=self.device)
+        if rewards_out is None:
+            rewards_out = torch.empty((K, self.n_envs), dtype=torch.int32, device=self.device)
+        nat.check(nat.lib.scg_bg_rollout(self._cfg_ref, self._st_ref, K, actions.data_ptr(), obs_out.data_ptr(),
+                                         rewards_out.data_ptr(), self._flags, self._stream()))
+        return obs_out, rewards_out
+
+    def poisson_demand(self, episode=None):
+        """The Poisson demand [T, N] the kernels draw for `episode` (default: current)."""
+        if self.demand_mode != nat.SCG_DEMAND_POISSON:
+            raise ValueError("env is not in poisson demand mode")
+        out = torch.empty((self.max_weeks, self.n_envs), dtype=torch.int32, device=self.device)
+        ep = self._st.episode if episode is None else int(episode)
+        nat.check(nat.lib.scg_bg_poisson_demand(self._cfg_ref, self._st_ref, ep, out.data_ptr(), self._stream()))
+        return out
+
+    # state views (device tensors, reference attribute names) -------------------------
+    @property
+    def week(self):
+        return self._st.week
+
+    @property
+    def episode(self):
+        return self._st.episode
+
+    @property
+    def env_offset(self):
+        return self._st.env_offset
+
+    @property
+    def seed_value(self):
+        return self._st.seed
+
+    @property
+    def inventory(self):
+        return self._inv
+
+    @property
+    def backlog(self):
+        return self._bk
+
+    @property
+    def orders_placed(self):
+        return self._op
+
+    @property
+    def inventory_costs(self):
+        return self._inv_costs
+
+    @property
+    def backlog_costs(self):
+        return self._bk_costs
+
+    @property
+    def all_orders_placed(self):
+        """[N, L, T+1] like the reference's all_orders_placed (:123, :151-152)."""
+        return None if self._hist is None else self._hist.permute(1, 2, 0)
+
+    @property
+    def episode_return(self):
+        return self._ret
+
+    @property
+    def final_return(self):
+        return self._final_ret
+
+    def close(self):
+        pass
+
+
+class BeerGameEnv:
+    """Drop-in for gym_supplychain.envs.BeerGameEnv (beergame_env.py:6-181), one env.
+
+    Same constructor, reset()/step()/render()/close() and NumPy return types: reset()
+    and step() give int64 observations, step() an np.int64 reward, a bool done and {}
+    (:138). Stepping past the last week raises IndexError (:79 on customer_demand[T]).
+    The week runs on the GPU as a batch of one; use BeerGameVecEnv for throughput.
+    """
+
+    def __init__(self, env_init_info={}, device=None):  # noqa: B006 - reference signature (:11)
+        self.DEBUG = False
+        self._vec = BeerGameVecEnv(1, env_init_info, demand="fixed", device=device, auto_reset=False,
+                                   track_costs=True, track_history=True, track_returns=False)
+        cfg = self._vec.config
+        self.levels = cfg.levels
+        self.inv_cost = cfg.inv_cost
+        self.backlog_cost = cfg.backlog_cost
+        self.customer_demand = cfg.customer_demand.astype(np.int64)
+        self.initial_inventory = cfg.initial_inventory.astype(np.int64)
+        self.max_weeks = cfg.max_weeks
+        self.shipment_delays = cfg.shipment_delays.astype(np.int64)
+        self.initial_shipment_value = cfg.initial_shipment_value
+        self.initial_orders_value = cfg.initial_orders_value
+        self.current_state = None
+        pin = torch.cuda.is_available()
+        self._act_host = torch.zeros((1, self.levels), dtype=torch.int32, pin_memory=pin)
+        self._act_np = self._act_host.numpy()
+        self._act_dev = torch.zeros((1, self.levels), dtype=torch.int32, device=self._vec.device)
+        self._out_host = torch.zeros(self._vec._out.shape, dtype=torch.int32, pin_memory=pin)
+        self._out_np = self._out_host.numpy()
+        self.week = None
+
+    def reset(self):
+        obs = self._vec.reset()
+        self.week = 0
+        self.current_state = obs[0].cpu().numpy().astype(np.int64)
+        return self.current_state
+
+    def step(self, action):
+        if self.week is None:  # the reference has no `week` before reset() (:67)
+            raise AttributeError("'BeerGameEnv' object has no attribute 'week' (call reset() first)")
+        a = np.asarray(action)
+        if a.dtype.kind == "f":
+            a = np.trunc(a)
+        self._act_np[0, :] = np.broadcast_to(a, (self.levels,))
+        self._act_dev.copy_(self._act_host, non_blocking=True)
+        obs, _, done, _ = self._vec.step(self._act_dev)
+        self._out_host.copy_(self._vec._out, non_blocking=True)
+        torch.cuda.current_stream(self._vec.device).synchronize()
+        L = self.levels
+        self.week = self._vec.week
+        self.current_state = self._out_np[:L].astype(np.int64)
+        reward = np.int64(self._out_np[L])
+        if self.DEBUG:
+            print('env.step()', self.current_state)
+        return self.current_state, reward, self.week == self.max_weeks, {}
+
+    # reference attributes, read back from the device on access
+    def _row(self, t):
+        return t[0].cpu().numpy().astype(np.int64)
+
+    @property
+    def inventory(self):
+        return self._row(self._vec.inventory)
+
+    @property
+    def backlog(self):
+        return self._row(self._vec.backlog)
+
+    @property
+    def orders_placed(self):
+        return self._row(self._vec.orders_placed)
+
+    @property
+    def inventory_costs(self):
+        return self._row(self._vec.inventory_costs)
+
+    @property
+    def backlog_costs(self):
+        return self._row(self._vec.backlog_costs)
+
+    @property
+    def all_orders_placed(self):
+        return self._vec.all_orders_placed[0].cpu().numpy().astype(np.int64)
+
+    def render(self, mode='human'):  # beergame_env.py:158-175 (the pipeline rows are not kept)
+        inv, bk = self.inventory, self.backlog
+        print('\n' + '=' * 20)
+        print('Week:\t', self.week)
+        print('Inventory:\t', inv, bk, inv - bk)
+        print('Orders placed:\t', self.orders_placed)
+        if self.week is not None and self.week < self.max_weeks:
+            print('Next customer demand:\t', self.customer_demand[self.week])
+        print('Inventory costs:\t', self.inventory_costs)
+        print('Backlog costs:\t', self.backlog_costs)
+
+    def close(self):
+        pass
+
+    def _observation(self):
+        return self.inventory - self.backlog

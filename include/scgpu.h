@@ -1,0 +1,186 @@
+/*
+ * scgpu — MI355X-native (gfx950) vectorised supply-chain environments: C ABI.
+ *
+ * This is the drop-in boundary for the hot path of caburu/gym-supplychain
+ * (reference snapshot 2024-08-07, mounted at /root/reference): the per-env
+ * step()/reset() dynamics of BeerGameEnv, run as fused HIP kernels over a batch of
+ * N envs held in caller-owned device buffers.
+ *
+ * The reference is pure Python; its "interface" for this path is the gym.Env
+ * surface of BeerGameEnv (gym_supplychain/envs/beergame_env.py):
+ *     __init__(env_init_info)  beergame_env.py:11-60   -> scg_bg_config + scg_bg_prepare
+ *     reset()                  beergame_env.py:140-156 -> scg_bg_reset
+ *     step(action)             beergame_env.py:66-138  -> scg_bg_step / scg_bg_rollout
+ *     _observation()           beergame_env.py:180-181 -> fused into the step epilogue
+ * The Python package gym_supplychain_amd binds these entry points with ctypes
+ *  and re-exposes the reference's class names and gym API.
+ *
+ * Conventions
+ *   - Every function returns an int status (scg_status). Nothing throws across the ABI.
+ *     On failure scg_last_error() describes the problem (thread-local).
+ *   - The library never allocates device memory and never synchronises: all buffers
+ *     are owned by the caller, every launch is asynchronous on the caller's stream
+ *     (`stream` is a hipStream_t passed as void*; NULL = the null stream).
+ *   - Integer state is int32; the reference's int64 values are reproduced exactly while
+ *     every value stays within int32 range (DESIGN.md "Integer range").
+ *   - Layouts are env-major: a [N][L] int32 array holds env n's L levels contiguously.
+ */
+#ifndef SCGPU_H
+#define SCGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCG_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define SCG_API __attribute__((visibility("default")))
+#else
+#define SCG_API
+#endif
+
+#define SCG_BG_MAX_LEVELS 16   /* template instantiations of the step kernel        */
+#define SCG_BG_MAX_WEEKS 4096  /* episode horizon (len(customer_demand), :37)        */
+#define SCG_BG_MAX_DELAY 63    /* shipment delay bound: ring slots R = max delay + 1 */
+#define SCG_POISSON_MAX 256    /* CDF threshold table entries                        */
+#define SCG_BG_ROLLOUT_MAX 128 /* weeks per rollout launch (host loops beyond)       */
+
+typedef enum scg_status {
+  SCG_OK = 0,
+  SCG_ERR_INVALID = 1,      /* bad argument or config              -> ValueError    */
+  SCG_ERR_PAST_HORIZON = 2, /* step after the terminal week        -> IndexError    */
+                            /* (the reference raises IndexError on customer_demand[T], :79) */
+  SCG_ERR_NOT_RESET = 3,    /* step before reset                   -> RuntimeError  */
+  SCG_ERR_HIP = 4           /* HIP launch/runtime error            -> RuntimeError  */
+} scg_status;
+
+typedef enum scg_demand_mode {
+  SCG_DEMAND_FIXED = 0,   /* one list shared by all envs: customer_demand (beergame_env.py:33) */
+  SCG_DEMAND_TABLE = 1,   /* per-env device table int32 [T][N] (caller-drawn demand)            */
+  SCG_DEMAND_POISSON = 2  /* per-(env, episode, week) Poisson draw on device, Philox4x32-10     */
+} scg_demand_mode;
+
+/* Step flags */
+#define SCG_BG_AUTORESET 1u /* at the terminal week reset in the same launch (VecEnv semantics) */
+
+/* Philox streams (counter word 3) */
+#define SCG_STREAM_DEMAND 0u
+#define SCG_STREAM_ACTION 1u
+
+/*
+ * Env configuration, the resolved form of BeerGameEnv's env_init_info
+ * (beergame_env.py:16-58). Host memory, owned by the caller.
+ */
+typedef struct scg_bg_config {
+  int32_t levels;                 /* L, :26                                            */
+  int32_t max_weeks;              /* T = len(customer_demand), :37                     */
+  int32_t inv_cost;               /* :28                                               */
+  int32_t backlog_cost;           /* :30                                               */
+  int32_t initial_shipment_value; /* :41                                               */
+  int32_t initial_orders_value;   /* :43                                               */
+  int32_t initial_inventory[SCG_BG_MAX_LEVELS]; /* :35                                 */
+  int32_t demand_mode;            /* scg_demand_mode                                   */
+  int32_t poisson_len;            /* entries in poisson_thresholds (POISSON mode)      */
+  const int32_t* shipment_delays; /* HOST [T+1]: [2] + user list, exactly :39          */
+  const int32_t* customer_demand; /* HOST [T]: FIXED mode demand, :33                  */
+  const int32_t* demand_table;    /* DEVICE [T][N]: TABLE mode demand                   */
+  const uint32_t* poisson_thresholds; /* DEVICE [poisson_len] (scg_poisson_table)       */
+  int32_t* plan;                  /* HOST [T+1] workspace, filled by scg_bg_prepare     */
+  int32_t ring_slots;             /* out of scg_bg_prepare: R = max delay + 1           */
+  int32_t reserved;
+} scg_bg_config;
+
+/*
+ * Batch state: caller-owned device buffers plus host-side counters the library
+ * advances. Optional buffers may be NULL (then that output is not produced).
+ */
+typedef struct scg_bg_state {
+  int64_t n_envs;           /* N envs in this shard                                   */
+  int64_t env_offset;       /* global id of env 0 of this shard (multi-GPU sharding)   */
+  uint64_t seed;            /* Philox key                                             */
+  uint32_t episode;         /* episode counter (Philox); advanced by reset/auto-reset  */
+  int32_t week;             /* 0 after reset, T at the terminal week; -1 = not reset   */
+  int32_t* inventory;       /* [N][L]  self.inventory      :72,:101                    */
+  int32_t* backlog;         /* [N][L]  self.backlog        :103                        */
+  int32_t* orders_placed;   /* [N][L]  self.orders_placed  :121                        */
+  int32_t* shipments;       /* [R][N][L] ring over absolute weeks (self.shipments :50)  */
+  int32_t* inventory_costs; /* [N][L]  self.inventory_costs :131   (optional)           */
+  int32_t* backlog_costs;   /* [N][L]  self.backlog_costs   :132   (optional)           */
+  int32_t* orders_history;  /* [T+1][N][L] self.all_orders_placed :123 (optional)       */
+  int64_t* episode_return;  /* [N] running sum of rewards (optional)                   */
+  int64_t* final_return;    /* [N] episode_return at the terminal week (optional)      */
+} scg_bg_state;
+
+/* ABI version (SCG_ABI_VERSION of the built library). */
+SCG_API int scg_abi_version(void);
+
+/* sizeof(scg_bg_config) and sizeof(scg_bg_state) as compiled, to check FFI bindings. */
+SCG_API int scg_bg_struct_sizes(size_t* config_size, size_t* state_size);
+
+/* Last error message of the calling thread ("" if none). */
+SCG_API const char* scg_last_error(void);
+
+/*
+ * Poisson(lam) inverse-CDF table: out[k] = min(floor(CDF(k) * 2^32), 2^32-1) for
+ * k = 0..len-1, ending at the first saturated entry. Returns len (>0) or -SCG_ERR_INVALID.
+ * Host function; the caller uploads the table for SCG_DEMAND_POISSON.
+ */
+SCG_API int scg_poisson_table(double lam, uint32_t* out, int32_t cap);
+
+/*
+ * Validate cfg and fill cfg->plan / cfg->ring_slots from cfg->shipment_delays
+ * (replaces the shipment-table sizing of beergame_env.py:46-52). Host only.
+ */
+SCG_API int scg_bg_prepare(scg_bg_config* cfg);
+
+/* reset() for all N envs (beergame_env.py:140-156). obs: DEVICE int32 [N][L] or NULL. */
+SCG_API int scg_bg_reset(const scg_bg_config* cfg, scg_bg_state* st, int32_t* obs, void* stream);
+
+/*
+ * step(action) for all N envs (beergame_env.py:66-138), one fused kernel.
+ *   action       DEVICE int32 [N][L]
+ *   obs          DEVICE int32 [N][L]   inventory - backlog (:127,:180); with
+ *                SCG_BG_AUTORESET at the terminal week: the reset observation
+ *   reward       DEVICE int32 [N]      -sum(inv_cost*inv + backlog_cost*backlog) (:130)
+ *   terminal_obs DEVICE int32 [N][L] or NULL: observation at the terminal week
+ * Returns SCG_ERR_PAST_HORIZON when called after the terminal week without auto-reset.
+ * Sets *done (host, may be NULL) to 1 when this step was the terminal week (:134).
+ */
+SCG_API int scg_bg_step(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* action,
+                int32_t* obs, int32_t* reward, int32_t* terminal_obs, uint32_t flags,
+                int32_t* done, void* stream);
+
+/*
+ * K consecutive steps in one launch per <= SCG_BG_ROLLOUT_MAX weeks, state held in
+ * registers/LDS (open-loop action plans, evaluation sweeps). Same results as K calls
+ * of scg_bg_step with the same flags (SCG_BG_AUTORESET may cross episode ends).
+ *   actions DEVICE int32 [K][N][L]; obs DEVICE int32 [K][N][L] or NULL;
+ *   rewards DEVICE int32 [K][N] or NULL.
+ */
+SCG_API int scg_bg_rollout(const scg_bg_config* cfg, scg_bg_state* st, int32_t n_weeks,
+                   const int32_t* actions, int32_t* obs, int32_t* rewards, uint32_t flags,
+                   void* stream);
+
+/*
+ * Device-side Philox draws for tests and benchmarks (no host round trip):
+ *  scg_bg_poisson_demand: out DEVICE int32 [T][N], the demand scg_bg_step draws
+ *    for episode `episode` in SCG_DEMAND_POISSON mode.
+ *  scg_uniform_ints: out DEVICE int32 [rows][N][width], uniform in [lo, hi],
+ *    word j of env n from philox(ctr=(env_offset+n, tag, j/4, SCG_STREAM_ACTION))[j%4]
+ *    with j = row*width + col.
+ */
+SCG_API int scg_bg_poisson_demand(const scg_bg_config* cfg, const scg_bg_state* st, uint32_t episode,
+                          int32_t* out, void* stream);
+SCG_API int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, int32_t rows,
+                     int32_t width, uint32_t tag, int32_t lo, int32_t hi, int32_t* out,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SCGPU_H */

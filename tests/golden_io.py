@@ -1,0 +1,24 @@
+"""Helpers to read tests/golden/beergame_*.npz (written by oracle/gen_golden.py)."""
+import glob
+import os
+
+import numpy as np
+
+from conftest import GOLDEN
+
+
+def beergame_cases():
+    return sorted(os.path.basename(p)[len("beergame_"):-4] for p in glob.glob(os.path.join(GOLDEN, "beergame_*.npz")))
+
+
+def load_beergame(name):
+    g = dict(np.load(os.path.join(GOLDEN, f"beergame_{name}.npz")))
+    L = int(g["levels"])
+    info = dict(levels=L, inv_cost=int(g["inv_cost"]), backlog_cost=int(g["backlog_cost"]),
+                initial_inventory=g["initial_inventory"].tolist(),
+                initial_shipment_value=int(g["initial_shipment_value"]),
+                initial_orders_value=int(g["initial_orders_value"]),
+                shipment_delays=g["shipment_delays"].tolist())
+    g["info"] = info
+    g["is_poisson"] = float(g["lam"]) >= 0
+    return g

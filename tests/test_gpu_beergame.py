@@ -1,0 +1,233 @@
+"""GPU parity: the HIP BeerGame kernels (through the C ABI) against the reference's golden
+vectors and, at full BASELINE sizes, against the oracle. Integer state must be bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import beergame_cases, load_beergame
+from oracle.beergame import run_batch_episode
+from oracle.philox import STREAM_ACTION, STREAM_DEMAND, draw_words
+from oracle.poisson import poisson_invert, poisson_thresholds
+
+pytestmark = pytest.mark.gpu
+CASES = beergame_cases()
+DEV = "cuda"
+
+
+def _vec(g, **kw):
+    from gym_supplychain_amd import BeerGameVecEnv
+    T, N, L = g["actions"].shape
+    if g["is_poisson"]:
+        env = BeerGameVecEnv(N, g["info"], demand="poisson", poisson_lambda=float(g["lam"]), seed=int(g["seed"]),
+                             horizon=T, device=DEV, **kw)
+        for _ in range(int(g["episode"])):  # each reset after the first starts the next episode
+            env.reset()
+    else:
+        env = BeerGameVecEnv(N, dict(g["info"], customer_demand=g["demand"][0].tolist()), demand="fixed",
+                             device=DEV, **kw)
+    return env
+
+
+def _i32(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.int32, device=DEV)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_step_matches_reference(name):
+    g = load_beergame(name)
+    T, N, L = g["actions"].shape
+    env = _vec(g, auto_reset=False, track_history=True)
+    obs = env.reset()
+    assert np.array_equal(obs.cpu().numpy(), g["ref_reset_obs"])
+    acts = _i32(g["actions"])
+    for w in range(T):
+        obs, rew, done, info = env.step(acts[w])
+        assert np.array_equal(obs.cpu().numpy(), g["ref_obs"][w]), (name, w)
+        assert np.array_equal(rew.cpu().numpy(), g["ref_reward"][w]), (name, w)
+        assert np.array_equal(env.inventory.cpu().numpy(), g["ref_inventory"][w])
+        assert np.array_equal(env.backlog.cpu().numpy(), g["ref_backlog"][w])
+        assert np.array_equal(env.orders_placed.cpu().numpy(), g["ref_orders_placed"][w])
+        assert bool(done.all()) == bool(g["ref_done"][w].all()) and bool(done.any()) == bool(g["ref_done"][w].any())
+    assert np.array_equal(env.inventory_costs.cpu().numpy(), g["ref_inventory_costs"])
+    assert np.array_equal(env.backlog_costs.cpu().numpy(), g["ref_backlog_costs"])
+    assert np.array_equal(env.all_orders_placed.cpu().numpy(), g["ref_all_orders_placed"])
+    assert np.array_equal(env.episode_return.cpu().numpy(), g["ref_reward"].astype(np.int64).sum(0))
+    assert np.array_equal(env.final_return.cpu().numpy(), g["ref_reward"].astype(np.int64).sum(0))
+    with pytest.raises(IndexError):  # the reference raises on customer_demand[T] (:79)
+        env.step(acts[0])
+
+
+@pytest.mark.parametrize("name", [c for c in CASES if c != "levels3_fixed"])
+def test_device_poisson_draws_match_oracle(name):
+    g = load_beergame(name)
+    env = _vec(g)
+    got = env.poisson_demand(int(g["episode"])).cpu().numpy().T
+    assert np.array_equal(got, g["demand"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_table_demand_and_rollout_match_reference(name):
+    from gym_supplychain_amd import BeerGameVecEnv
+    g = load_beergame(name)
+    T, N, L = g["actions"].shape
+    env = BeerGameVecEnv(N, g["info"], demand=_i32(g["demand"].T), device=DEV, auto_reset=False,
+                         track_history=True)
+    env.reset()
+    obs, rew = env.rollout(_i32(g["actions"]))
+    assert np.array_equal(obs.cpu().numpy(), g["ref_obs"])
+    assert np.array_equal(rew.cpu().numpy(), g["ref_reward"])
+    assert np.array_equal(env.inventory.cpu().numpy(), g["ref_inventory"][-1])
+    assert np.array_equal(env.backlog.cpu().numpy(), g["ref_backlog"][-1])
+    assert np.array_equal(env.orders_placed.cpu().numpy(), g["ref_orders_placed"][-1])
+    assert np.array_equal(env.inventory_costs.cpu().numpy(), g["ref_inventory_costs"])
+    assert np.array_equal(env.backlog_costs.cpu().numpy(), g["ref_backlog_costs"])
+    assert np.array_equal(env.all_orders_placed.cpu().numpy(), g["ref_all_orders_placed"])
+    with pytest.raises(IndexError):
+        env.rollout(_i32(g["actions"][:1]))
+
+
+@pytest.mark.parametrize("name", ["levels3_fixed", "vardelay_negact", "levels1"])
+def test_single_env_facade(name):
+    from gym_supplychain_amd import BeerGameEnv
+    g = load_beergame(name)
+    T, N, L = g["actions"].shape
+    for n in range(3):
+        env = BeerGameEnv(dict(g["info"], customer_demand=g["demand"][n].tolist()))
+        with pytest.raises(AttributeError):
+            env.step(np.zeros(L, dtype=np.int64))
+        o = env.reset()
+        assert o.dtype == np.int64 and np.array_equal(o, g["ref_reset_obs"][n])
+        for w in range(T):
+            obs, r, done, info = env.step(g["actions"][w, n].tolist())
+            assert obs.dtype == np.int64 and isinstance(r, np.int64) and isinstance(done, bool) and info == {}
+            assert np.array_equal(obs, g["ref_obs"][w, n]) and r == g["ref_reward"][w, n]
+            assert done == bool(g["ref_done"][w, n])
+        assert np.array_equal(env.inventory_costs, g["ref_inventory_costs"][n])
+        assert np.array_equal(env.all_orders_placed, g["ref_all_orders_placed"][n])
+        with pytest.raises(IndexError):
+            env.step(g["actions"][0, n])
+
+
+def _oracle_episode(info, N, T, L, seed, lam, episode, actions, env_offset=0):
+    thr = poisson_thresholds(lam)
+    words = draw_words(seed, np.arange(env_offset, env_offset + N), episode, T, STREAM_DEMAND)
+    demand = poisson_invert(words, thr)
+    return run_batch_episode(info, demand, actions)
+
+
+def _uniform_actions_np(seed, N, T, L, tag, lo, hi, env_offset=0):
+    words = draw_words(seed, np.arange(env_offset, env_offset + N), tag, T * L, STREAM_ACTION)
+    v = lo + ((words.astype(np.uint64) * np.uint64(hi - lo + 1)) >> np.uint64(32)).astype(np.int64)
+    return v.reshape(N, T, L).transpose(1, 0, 2)
+
+
+def _uniform_actions_dev(seed, N, T, L, tag, lo, hi, env_offset=0):
+    import ctypes
+    from gym_supplychain_amd import _native as nat
+    out = torch.empty((T, N, L), dtype=torch.int32, device=DEV)
+    nat.check(nat.lib.scg_uniform_ints(seed, env_offset, N, T, L, tag, lo, hi, out.data_ptr(),
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    return out
+
+
+def test_full_size_episode_matches_oracle():
+    """BASELINE config 2 at full size: 65,536 envs, Poisson(8) demand, default chain."""
+    from gym_supplychain_amd import BeerGameVecEnv
+    N, T, L, seed, lam = 65536, 35, 4, 0x5EED0000, 8.0
+    acts = _uniform_actions_dev(seed, N, T, L, 0, 0, 8)
+    acts_np = _uniform_actions_np(seed, N, T, L, 0, 0, 8)
+    assert np.array_equal(acts.cpu().numpy(), acts_np)
+    env = BeerGameVecEnv(N, {}, demand="poisson", poisson_lambda=lam, seed=seed, device=DEV, auto_reset=False,
+                         track_history=True)
+    env.reset()
+    want = _oracle_episode({}, N, T, L, seed, lam, 0, acts_np)
+    obs_all = np.zeros((T, N, L), dtype=np.int64)
+    rew_all = np.zeros((T, N), dtype=np.int64)
+    for w in range(T):
+        obs, rew, done, _ = env.step(acts[w])
+        obs_all[w] = obs.cpu().numpy()
+        rew_all[w] = rew.cpu().numpy()
+    assert np.array_equal(obs_all, want["obs"])
+    assert np.array_equal(rew_all, want["reward"])
+    assert np.array_equal(env.inventory_costs.cpu().numpy(), want["inventory_costs"])
+    assert np.array_equal(env.backlog_costs.cpu().numpy(), want["backlog_costs"])
+    assert np.array_equal(env.all_orders_placed.cpu().numpy(), want["all_orders_placed"])
+    # size-independent property: the return is the sum of the per-step rewards
+    assert np.array_equal(env.final_return.cpu().numpy(), want["reward"].sum(0))
+
+
+def test_autoreset_across_episodes_matches_oracle():
+    from gym_supplychain_amd import BeerGameVecEnv
+    N, T, L, seed, lam = 4096, 35, 4, 17, 8.0
+    info = dict(shipment_delays=[1, 3, 0, 2] * 9)
+    env = BeerGameVecEnv(N, info, demand="poisson", poisson_lambda=lam, seed=seed, device=DEV, auto_reset=True)
+    obs0 = env.reset().clone()
+    for ep in range(3):
+        acts_np = _uniform_actions_np(seed, N, T, L, ep, -2, 9)
+        acts = _i32(acts_np)
+        want = _oracle_episode(info, N, T, L, seed, lam, ep, acts_np)
+        for w in range(T):
+            obs, rew, done, info_d = env.step(acts[w])
+            assert np.array_equal(rew.cpu().numpy(), want["reward"][w]), (ep, w)
+            if w < T - 1:
+                assert not bool(done.any()) and info_d == {}
+                assert np.array_equal(obs.cpu().numpy(), want["obs"][w])
+            else:
+                assert bool(done.all())
+                assert np.array_equal(info_d["terminal_observation"].cpu().numpy(), want["obs"][w])
+                assert np.array_equal(info_d["episode_return"].cpu().numpy(), want["reward"].sum(0))
+                assert np.array_equal(obs.cpu().numpy(), obs0.cpu().numpy())  # reset observation
+        assert env.week == 0 and env.episode == ep + 1
+
+
+def test_rollout_equals_steps_across_episode_end():
+    from gym_supplychain_amd import BeerGameVecEnv
+    N, T, L, seed = 3000, 12, 5, 5
+    info = dict(levels=L, initial_inventory=[12, 8, 4, 9, 1], customer_demand=[0] * T,
+                shipment_delays=[2, 0, 3, 1, 1, 4, 2, 0, 5, 1, 2, 3])
+    K = 3 * T + 5
+    acts = _uniform_actions_dev(seed, N, K, L, 7, -3, 7)
+    a = BeerGameVecEnv(N, info, demand="poisson", poisson_lambda=6.0, seed=seed, device=DEV)
+    b = BeerGameVecEnv(N, info, demand="poisson", poisson_lambda=6.0, seed=seed, device=DEV)
+    a.reset()
+    b.reset()
+    obs_r, rew_r = b.rollout(acts)
+    for k in range(K):
+        obs, rew, _, _ = a.step(acts[k])
+        assert torch.equal(obs, obs_r[k]) and torch.equal(rew, rew_r[k]), k
+    for t in ("inventory", "backlog", "orders_placed", "inventory_costs", "backlog_costs", "episode_return",
+              "final_return"):
+        assert torch.equal(getattr(a, t), getattr(b, t)), t
+    assert (a.week, a.episode) == (b.week, b.episode)
+
+
+def test_sharding_is_invariant():
+    """Rank shards (env_offset) reproduce one big batch bit for bit (DESIGN.md multi-GPU)."""
+    from gym_supplychain_amd import BeerGameVecEnv
+    N, T, L, seed = 2000, 35, 4, 3
+    acts = _uniform_actions_dev(seed, N, T, L, 0, 0, 8)
+    whole = BeerGameVecEnv(N, {}, demand="poisson", seed=seed, device=DEV)
+    parts = [BeerGameVecEnv(N // 2, {}, demand="poisson", seed=seed, env_offset=o, device=DEV) for o in (0, N // 2)]
+    whole.reset()
+    for p in parts:
+        p.reset()
+    for w in range(T):
+        o, r, _, _ = whole.step(acts[w])
+        o1, r1, _, _ = parts[0].step(acts[w, : N // 2])
+        o2, r2, _, _ = parts[1].step(acts[w, N // 2:])
+        assert torch.equal(o, torch.cat([o1, o2])) and torch.equal(r, torch.cat([r1, r2]))
+
+
+def test_errors():
+    from gym_supplychain_amd import BeerGameVecEnv
+    env = BeerGameVecEnv(8, {}, device=DEV)
+    with pytest.raises(RuntimeError):
+        env.step(torch.zeros((8, 4), dtype=torch.int32, device=DEV))
+    env.reset()
+    with pytest.raises(ValueError):
+        env.step(torch.zeros((8, 5), dtype=torch.int32, device=DEV))
+    with pytest.raises(ValueError):
+        BeerGameVecEnv(8, {}, demand="poisson", poisson_lambda=-1.0, device=DEV)
+    with pytest.raises(ValueError):
+        BeerGameVecEnv(8, {"shipment_delays": [99] * 35}, device=DEV)

@@ -1,0 +1,73 @@
+"""The BeerGame oracle restatements against golden vectors produced by the reference.
+
+tests/golden/beergame_*.npz were written by oracle/gen_golden.py, which ran the real
+gym_supplychain BeerGameEnv (beergame_env.py) in the build container. These tests pin
+the oracle that the GPU parity tests then use at sizes the golden files do not cover.
+"""
+import numpy as np
+import pytest
+
+from golden_io import beergame_cases, load_beergame
+from oracle.beergame import BeerGameOracle, run_batch_episode
+from oracle.philox import STREAM_DEMAND, draw_words
+from oracle.poisson import poisson_invert, poisson_thresholds
+
+CASES = beergame_cases()
+FIELDS = ["obs", "inventory", "backlog", "orders_placed", "reward", "inventory_costs", "backlog_costs",
+          "all_orders_placed", "reset_obs"]
+
+
+def test_golden_present():
+    assert {"default_poisson", "vardelay_negact", "delay_collide", "levels3_fixed", "levels6_short",
+            "levels1"} <= set(CASES)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_batch_oracle_matches_reference(name):
+    g = load_beergame(name)
+    out = run_batch_episode(g["info"], g["demand"], g["actions"])
+    for f in FIELDS:
+        assert np.array_equal(out[f], g["ref_" + f]), f
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_single_env_oracle_matches_reference(name):
+    g = load_beergame(name)
+    T, N, L = g["actions"].shape
+    for n in range(min(N, 6)):
+        env = BeerGameOracle(dict(g["info"], customer_demand=g["demand"][n].tolist()))
+        assert np.array_equal(env.reset(), g["ref_reset_obs"][n])
+        for w in range(T):
+            obs, r, done, info = env.step(g["actions"][w, n].astype(np.int64))
+            assert np.array_equal(obs, g["ref_obs"][w, n])
+            assert r == g["ref_reward"][w, n] and done == g["ref_done"][w, n] and info == {}
+        assert g["ref_past_horizon_raises"][n]
+        with pytest.raises(IndexError):
+            env.step(np.zeros(L, dtype=np.int64))
+
+
+@pytest.mark.parametrize("name", [c for c in CASES if c != "levels3_fixed"])
+def test_golden_demand_is_philox_poisson(name):
+    """The golden demand tables are the Philox/Poisson draws the device makes."""
+    g = load_beergame(name)
+    thr = poisson_thresholds(float(g["lam"]))
+    assert np.array_equal(thr, g["poisson_thresholds"])
+    N, T = g["demand"].shape
+    words = draw_words(int(g["seed"]), np.arange(N), int(g["episode"]), T, STREAM_DEMAND)
+    assert np.array_equal(poisson_invert(words, thr), g["demand"])
+
+
+def test_poisson_distribution():
+    lam = 8.0
+    thr = poisson_thresholds(lam)
+    words = draw_words(99, np.arange(4096), 0, 64, STREAM_DEMAND)
+    x = poisson_invert(words, thr)
+    assert abs(x.mean() - lam) < 0.05 and abs(x.var() - lam) < 0.2
+
+
+def test_poisson_table_edges():
+    assert poisson_thresholds(0.0).tolist() == [0xFFFFFFFF]
+    with pytest.raises(ValueError):
+        poisson_thresholds(-1.0)
+    with pytest.raises(ValueError):
+        poisson_thresholds(1000.0)
