@@ -13,6 +13,7 @@
 // whether the scheduled slot is written fresh (store) or accumulated (read-modify-write),
 // so the common constant-delay case moves exactly one due row in and one row out.
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -168,9 +169,11 @@ __global__ __launch_bounds__(kBlock) void bg_reset_kernel(const BgArgs a) {
   reset_env<L>(a, n, a.obs);
 }
 
-// One week of one env (beergame_env.py:66-138) on registers. `ship` rows go to the ring
-// (or straight into inventory when the week's delay is 0). Shared by the step kernel
-// (state from/to HBM each launch) and the rollout kernel (state held in registers).
+// One week of one env (beergame_env.py:66-138), pure register arithmetic. The caller
+// moves the rows: `due` is the pipeline row arriving this week (zeros when none), `ship`
+// comes back as the row scheduled `delay` weeks ahead (or is already added into the
+// inventory when the week's delay is 0, `direct`). Shared by the step kernel (state
+// from/to HBM every launch) and the rollout kernel (state held in registers).
 struct WeekInfo {
   int32_t week;        // 1..T
   int32_t read_slot;   // -1: nothing due
@@ -181,97 +184,93 @@ struct WeekInfo {
 };
 
 template <int L>
-__device__ __forceinline__ int32_t step_core(const BgArgs& a, int64_t n, const WeekInfo& wk, uint32_t episode,
-                                             int32_t (&inv)[L], int32_t (&bk)[L], int32_t (&op)[L],
-                                             const int32_t (&act)[L], int32_t (&obs)[L], int32_t (&ic)[L],
-                                             int32_t (&bc)[L]) {
-  const int64_t row = n * L;
-  const int64_t stride = a.n * L;
+__device__ __forceinline__ int32_t step_core(int32_t h, int32_t b, int32_t demand, bool direct,
+                                             const int32_t (&due)[L], int32_t (&inv)[L], int32_t (&bk)[L],
+                                             int32_t (&op)[L], const int32_t (&act)[L], int32_t (&ship)[L],
+                                             int32_t (&obs)[L], int32_t (&ic)[L], int32_t (&bc)[L]) {
   // 1. receive the shipments due this week (:72)
-  if (wk.read_slot >= 0) {
-    int32_t due[L];
-    load_row<L>(a.ring + wk.read_slot * stride + row, due);
-#pragma unroll
-    for (int l = 0; l < L; ++l) inv[l] += due[l];
-  }
   // 2. order slips: customer demand at level 0, the previous orders above (:79-81)
   int32_t inc[L];
-  inc[0] = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, episode);
+  inc[0] = demand;
 #pragma unroll
   for (int l = 1; l < L; ++l) inc[l] = op[l - 1];
-  // fill what inventory allows (:85-89)
+  // fill what inventory allows (:85-89); ship[l] = what level l receives: deliver[l+1]
+  // from the level above it, and for the factory its own orders_placed[-1] from before
+  // this step (:93-96, :111-114)
   int32_t fill[L], del[L];
 #pragma unroll
   for (int l = 0; l < L; ++l) {
+    inv[l] += due[l];
     fill[l] = inc[l] + bk[l];
     del[l] = min(inv[l], fill[l]);
   }
-  // ship downstream deliveries and the factory's previous order (:93-96, :111-114):
-  // ship[l] = what level l receives: deliver[l+1] from the level above it, and for the
-  // factory its own orders_placed[-1] from before this step.
-  int32_t ship[L];
 #pragma unroll
   for (int l = 0; l + 1 < L; ++l) ship[l] = del[l + 1];
   ship[L - 1] = op[L - 1];
-  if (wk.mode == MODE_DIRECT) {
-#pragma unroll
-    for (int l = 0; l < L; ++l) inv[l] += ship[l];
-  } else if (wk.mode == MODE_STORE) {
-    store_row<L>(a.ring + wk.write_slot * stride + row, ship);
-  } else if (wk.mode == MODE_ADD) {
-    int32_t* p = a.ring + wk.write_slot * stride + row;
-    int32_t cur[L];
-    load_row<L>(p, cur);
-#pragma unroll
-    for (int l = 0; l < L; ++l) cur[l] += ship[l];
-    store_row<L>(p, cur);
-  }  // MODE_DROP: arrives after the horizon, never observable
   // 3. inventory / backlog (:101-103); 5. place orders (:121); obs (:127,:180); cost (:130)
   int32_t cost = 0;
 #pragma unroll
   for (int l = 0; l < L; ++l) {
-    inv[l] -= del[l];
+    inv[l] += (direct ? ship[l] : 0) - del[l];
     bk[l] = fill[l] - del[l];
     op[l] = inc[l] + act[l];
     obs[l] = inv[l] - bk[l];
-    ic[l] = a.h * inv[l];
-    bc[l] = a.b * bk[l];
+    ic[l] = h * inv[l];
+    bc[l] = b * bk[l];
     cost += ic[l] + bc[l];
   }
-  if (a.hist) store_row<L>(a.hist + static_cast<int64_t>(wk.week) * stride + row, op);  // :123
   return -cost;
 }
 
 template <int L>
-__device__ __forceinline__ void add_row(int32_t* __restrict__ p, const int32_t (&v)[L]) {
-  int32_t acc[L];
-  load_row<L>(p, acc);
+__device__ __forceinline__ void zero_row(int32_t (&v)[L]) {
 #pragma unroll
-  for (int l = 0; l < L; ++l) acc[l] += v[l];
-  store_row<L>(p, acc);
+  for (int l = 0; l < L; ++l) v[l] = 0;
 }
 
-// step(action) for one env per lane: state in from HBM, one week, state out.
+// step(action) for one env per lane: every row this launch reads is loaded up front (one
+// round of memory latency), the week is computed in registers, then every row is stored.
 template <int L>
 __global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const WeekInfo wk) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (n >= a.n) return;
   const int64_t row = n * L;
-  int32_t inv[L], bk[L], op[L], act[L], obs[L], ic[L], bc[L];
+  const int64_t stride = a.n * L;
+  const bool terminal = wk.flags & 1;
+  const bool autoreset = wk.flags & 2;
+
+  int32_t inv[L], bk[L], op[L], act[L], due[L], cur[L], iacc[L], bacc[L];
   load_row<L>(a.inv + row, inv);
   load_row<L>(a.bk + row, bk);
   load_row<L>(a.op + row, op);
   load_row<L>(a.act + row, act);
-  const int32_t reward = step_core<L>(a, n, wk, a.episode, inv, bk, op, act, obs, ic, bc);
+  zero_row<L>(due);
+  zero_row<L>(cur);
+  zero_row<L>(iacc);
+  zero_row<L>(bacc);
+  if (wk.read_slot >= 0) load_row<L>(a.ring + wk.read_slot * stride + row, due);
+  if (wk.mode == MODE_ADD) load_row<L>(a.ring + wk.write_slot * stride + row, cur);
+  if (!autoreset && a.inv_acc) load_row<L>(a.inv_acc + row, iacc);
+  if (!autoreset && a.bk_acc) load_row<L>(a.bk_acc + row, bacc);
+  const int64_t ret0 = a.ep_ret ? a.ep_ret[n] : 0;
+  const int32_t demand = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, a.episode);
+
+  int32_t ship[L], obs[L], ic[L], bc[L];
+  const int32_t reward = step_core<L>(a.h, a.b, demand, wk.mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
+
+  if (wk.mode == MODE_STORE) {
+    store_row<L>(a.ring + wk.write_slot * stride + row, ship);
+  } else if (wk.mode == MODE_ADD) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) cur[l] += ship[l];
+    store_row<L>(a.ring + wk.write_slot * stride + row, cur);
+  }  // MODE_DROP: arrives after the horizon, never observable
   a.rew[n] = reward;
-  const bool terminal = wk.flags & 1;
+  if (a.hist) store_row<L>(a.hist + static_cast<int64_t>(wk.week) * stride + row, op);  // :123
   if (terminal && a.term_obs) store_row<L>(a.term_obs + row, obs);
-  if (a.ep_ret) {
-    const int64_t r = a.ep_ret[n] + reward;
-    if (terminal && a.final_ret) a.final_ret[n] = r;
-    a.ep_ret[n] = r;
-  }
-  if (wk.flags & 2) {  // auto-reset: the next step starts a fresh episode
+  const int64_t ret = ret0 + reward;
+  if (terminal && a.final_ret) a.final_ret[n] = ret;
+  if (autoreset) {  // the next step starts a fresh episode (reset() in the same launch)
     reset_env<L>(a, n, a.obs);
     return;
   }
@@ -279,12 +278,22 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const W
   store_row<L>(a.bk + row, bk);
   store_row<L>(a.op + row, op);
   store_row<L>(a.obs + row, obs);
-  if (a.inv_acc) add_row<L>(a.inv_acc + row, ic);  // :131
-  if (a.bk_acc) add_row<L>(a.bk_acc + row, bc);    // :132
+  if (a.inv_acc) {  // :131
+#pragma unroll
+    for (int l = 0; l < L; ++l) iacc[l] += ic[l];
+    store_row<L>(a.inv_acc + row, iacc);
+  }
+  if (a.bk_acc) {  // :132
+#pragma unroll
+    for (int l = 0; l < L; ++l) bacc[l] += bc[l];
+    store_row<L>(a.bk_acc + row, bacc);
+  }
+  if (a.ep_ret) a.ep_ret[n] = ret;
 }
 
 // K weeks per launch, inventory/backlog/orders/ledgers/return in registers; only the
-// pipeline ring (RMW through L2), actions in and obs/rewards out touch memory per week.
+// pipeline ring (read-modify-write through L2), actions in and obs/rewards out touch
+// memory per week.
 struct RolloutWeeks {
   WeekInfo wk[SCG_BG_ROLLOUT_MAX];
 };
@@ -301,17 +310,30 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int3
   load_row<L>(a.inv + row, inv);
   load_row<L>(a.bk + row, bk);
   load_row<L>(a.op + row, op);
-#pragma unroll
-  for (int l = 0; l < L; ++l) iacc[l] = bacc[l] = 0;
+  zero_row<L>(iacc);
+  zero_row<L>(bacc);
   if (a.inv_acc) load_row<L>(a.inv_acc + row, iacc);
   if (a.bk_acc) load_row<L>(a.bk_acc + row, bacc);
   int64_t ret = a.ep_ret ? a.ep_ret[n] : 0;
   uint32_t episode = a.episode;
   for (int32_t k = 0; k < K; ++k) {
     const WeekInfo wk = weeks.wk[k];
-    int32_t act[L], obs[L], ic[L], bc[L];
+    int32_t act[L], due[L], obs[L], ic[L], bc[L], ship[L];
     load_row<L>(acts + k * stride + row, act);
-    const int32_t reward = step_core<L>(a, n, wk, episode, inv, bk, op, act, obs, ic, bc);
+    zero_row<L>(due);
+    if (wk.read_slot >= 0) load_row<L>(a.ring + wk.read_slot * stride + row, due);
+    const int32_t demand = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, episode);
+    const int32_t reward = step_core<L>(a.h, a.b, demand, wk.mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
+    if (wk.mode == MODE_STORE) {
+      store_row<L>(a.ring + wk.write_slot * stride + row, ship);
+    } else if (wk.mode == MODE_ADD) {
+      int32_t cur[L];
+      load_row<L>(a.ring + wk.write_slot * stride + row, cur);
+#pragma unroll
+      for (int l = 0; l < L; ++l) cur[l] += ship[l];
+      store_row<L>(a.ring + wk.write_slot * stride + row, cur);
+    }
+    if (a.hist) store_row<L>(a.hist + static_cast<int64_t>(wk.week) * stride + row, op);
     ret += reward;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
@@ -388,9 +410,12 @@ int launch_reset(int L, dim3 grid, hipStream_t s, const BgArgs& a) {
   return check_launch("bg_reset_kernel");
 }
 
-int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk) {
+int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk, hipEvent_t ev0,
+                hipEvent_t ev1) {
+  // hipExtLaunchKernelGGL ties the optional events to this dispatch's own start/end
+  // timestamps (the numbers rocprofv3 reports), not to separate event packets.
   switch (L) {
-#define X(l) case l: hipLaunchKernelGGL(bg_step_kernel<l>, grid, dim3(kBlock), 0, s, a, wk); break;
+#define X(l) case l: hipExtLaunchKernelGGL(bg_step_kernel<l>, grid, dim3(kBlock), 0, s, ev0, ev1, 0, a, wk); break;
     SCG_LEVEL_CASES(X)
 #undef X
     default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
@@ -569,6 +594,12 @@ static int check_step(const scg_bg_config* cfg, const scg_bg_state* st) {
 
 int scg_bg_step(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* action, int32_t* obs,
                 int32_t* reward, int32_t* terminal_obs, uint32_t flags, int32_t* done, void* stream) {
+  return scg_bg_step_timed(cfg, st, action, obs, reward, terminal_obs, flags, done, nullptr, nullptr, stream);
+}
+
+int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* action, int32_t* obs,
+                      int32_t* reward, int32_t* terminal_obs, uint32_t flags, int32_t* done, void* start_event,
+                      void* stop_event, void* stream) {
   if (int rc = check_state(cfg, st)) return rc;
   if (!action || !obs || !reward) return fail(SCG_ERR_INVALID, "action/obs/reward buffers are required");
   if (int rc = check_step(cfg, st)) return rc;
@@ -579,7 +610,9 @@ int scg_bg_step(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* actio
   a.obs = obs;
   a.rew = reward;
   a.term_obs = terminal_obs;
-  if (int rc = launch_step(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a, wk)) return rc;
+  if (int rc = launch_step(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a, wk,
+                           static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event)))
+    return rc;
   if (wk.flags & 2) {
     st->week = 0;
     st->episode += 1;

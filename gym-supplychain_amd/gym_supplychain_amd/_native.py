@@ -97,6 +97,9 @@ SIGNATURES = {
     "scg_bg_step": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                    _i32p, ctypes.c_void_p]),
+    "scg_bg_step_timed": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                         _i32p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "scg_bg_rollout": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p]),
@@ -159,6 +162,53 @@ def poisson_table(lam):
     if n < 0:
         check(-n)
     return list(buf[:n])
+
+
+try:  # the raw hipStream_t of torch's current stream without building a Stream object
+    _raw_stream = torch._C._cuda_getCurrentRawStream
+except AttributeError:  # pragma: no cover - older torch
+    _raw_stream = None
+
+
+def raw_stream(device_index):
+    if _raw_stream is not None:
+        return _raw_stream(device_index)
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
+_hip = None
+
+
+def hip_runtime():
+    """The HIP runtime library torch loaded (so events/streams are shared handles)."""
+    global _hip
+    if _hip is None:
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        _hip = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so.7")
+        _hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        _hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        _hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+    return _hip
+
+
+def hip_event():
+    """A new timing-enabled hipEvent_t (int handle) from torch's HIP runtime."""
+    h = ctypes.c_void_p()
+    if hip_runtime().hipEventCreate(ctypes.byref(h)) != 0:
+        raise RuntimeError("hipEventCreate failed")
+    return h.value
+
+
+def hip_event_elapsed_ms(start, stop):
+    ms = ctypes.c_float()
+    rc = hip_runtime().hipEventElapsedTime(ctypes.byref(ms), start, stop)
+    if rc != 0:
+        raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
+    return ms.value
+
+
+def hip_event_destroy(ev):
+    hip_runtime().hipEventDestroy(ev)
 
 
 def stream_handle(device=None):

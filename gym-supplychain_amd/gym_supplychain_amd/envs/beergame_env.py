@@ -115,9 +115,12 @@ class BeerGameVecEnv:
         n_envs = int(n_envs)
         if n_envs < 1:
             raise ValueError("n_envs must be >= 1")
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type != "cuda":
             raise ValueError("BeerGameVecEnv runs on a GPU device (no CPU fallback)")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self._dev_index = self.device.index
         table = None
         if isinstance(demand, torch.Tensor):
             table = demand
@@ -205,7 +208,13 @@ class BeerGameVecEnv:
         self._cfg_ref = ctypes.byref(self._cfg)
         self._st_ref = ctypes.byref(self._st)
         self._done_flag = ctypes.c_int32(0)
+        self._done_ref = ctypes.byref(self._done_flag)
         self._flags = nat.SCG_BG_AUTORESET if self.auto_reset else 0
+        self._act_shape = (n_envs, L)
+        self._obs_ptr, self._rew_ptr = self._obs.data_ptr(), self._rew.data_ptr()
+        self._term_ptr = self._term_obs.data_ptr()
+        self._step_fn = nat.lib.scg_bg_step
+        self._step_timed_fn = nat.lib.scg_bg_step_timed
         # gym surface (an extension: the reference leaves both spaces unset, :62-64)
         self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
         self.single_action_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
@@ -214,7 +223,7 @@ class BeerGameVecEnv:
 
     # -------------------------------------------------------------------------------
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return nat.raw_stream(self._dev_index)
 
     def reset(self):
         nat.check(nat.lib.scg_bg_reset(self._cfg_ref, self._st_ref, self._obs.data_ptr(), self._stream()))
@@ -234,11 +243,20 @@ class BeerGameVecEnv:
             actions = actions.reshape(N, L)
         return actions.contiguous()
 
-    def step(self, actions):
-        act = self._actions(actions)
-        rc = nat.lib.scg_bg_step(self._cfg_ref, self._st_ref, act.data_ptr(), self._obs.data_ptr(),
-                                 self._rew.data_ptr(), self._term_obs.data_ptr(), self._flags,
-                                 ctypes.byref(self._done_flag), self._stream())
+    def _is_ready(self, a):
+        return (type(a) is torch.Tensor and a.dtype is torch.int32 and a.is_cuda
+                and a.get_device() == self._dev_index and a.shape == self._act_shape and a.is_contiguous())
+
+    def step(self, actions, _events=None):
+        if not self._is_ready(actions):
+            actions = self._actions(actions)
+        if _events is None:
+            rc = self._step_fn(self._cfg_ref, self._st_ref, actions.data_ptr(), self._obs_ptr, self._rew_ptr,
+                               self._term_ptr, self._flags, self._done_ref, nat.raw_stream(self._dev_index))
+        else:  # (start, stop) hipEvent_t handles stamped with the kernel's own dispatch times
+            rc = self._step_timed_fn(self._cfg_ref, self._st_ref, actions.data_ptr(), self._obs_ptr, self._rew_ptr,
+                                     self._term_ptr, self._flags, self._done_ref, _events[0], _events[1],
+                                     nat.raw_stream(self._dev_index))
         if rc:
             nat.check(rc)
         if self._done_flag.value:

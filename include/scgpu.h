@@ -155,6 +155,16 @@ SCG_API int scg_bg_step(const scg_bg_config* cfg, scg_bg_state* st, const int32_
                 int32_t* done, void* stream);
 
 /*
+ * scg_bg_step with the step kernel's own dispatch timestamps recorded into two
+ * caller-created hipEvent_t (passed as void*, either may be NULL), via
+ * hipExtLaunchKernel: hipEventElapsedTime(start, stop) is the kernel's duration as
+ * rocprofv3 reports it. Used by bench.py for the roofline's measured kernel time.
+ */
+SCG_API int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* action,
+                              int32_t* obs, int32_t* reward, int32_t* terminal_obs, uint32_t flags,
+                              int32_t* done, void* start_event, void* stop_event, void* stream);
+
+/*
  * K consecutive steps in one launch per <= SCG_BG_ROLLOUT_MAX weeks, state held in
  * registers/LDS (open-loop action plans, evaluation sweeps). Same results as K calls
  * of scg_bg_step with the same flags (SCG_BG_AUTORESET may cross episode ends).

@@ -1,0 +1,52 @@
+"""Multi-process sharding logic on CPU (gloo, world_size 2): env-id offsets and the
+end-of-episode return all-gather used by bench.py at N > 1."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gym_supplychain_amd.distributed import EpisodeReturnGather, rank_world, shard_offset
+        assert rank_world() == (rank, world)
+        g = EpisodeReturnGather(n, "cpu")
+        out = []
+        for ep in range(3):
+            final = torch.arange(n, dtype=torch.int64) + 1000 * rank + 100000 * ep
+            g.on_episode_end(final)
+            out.append(g.result().clone())
+        q.put((rank, shard_offset(n), [o.tolist() for o in out], g.gathers))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_episode_return_allgather_gloo():
+    pytest.importorskip("torch.distributed")
+    world, n = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, off, outs, gathers in res:
+        assert off == rank * n and gathers == 3
+        for ep, o in enumerate(outs):
+            want = [i + 1000 * r + 100000 * ep for r in range(world) for i in range(n)]
+            assert o == want

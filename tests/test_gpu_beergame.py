@@ -231,3 +231,25 @@ def test_errors():
         BeerGameVecEnv(8, {}, demand="poisson", poisson_lambda=-1.0, device=DEV)
     with pytest.raises(ValueError):
         BeerGameVecEnv(8, {"shipment_delays": [99] * 35}, device=DEV)
+
+
+def test_timed_step_matches_and_stamps_kernel():
+    from gym_supplychain_amd import BeerGameVecEnv
+    from gym_supplychain_amd import _native as nat
+    N, T, L = 4096, 35, 4
+    acts = _uniform_actions_dev(1, N, T, L, 0, 0, 8)
+    a = BeerGameVecEnv(N, {}, demand="poisson", seed=1, device=DEV)
+    b = BeerGameVecEnv(N, {}, demand="poisson", seed=1, device=DEV)
+    a.reset()
+    b.reset()
+    evs = [(nat.hip_event(), nat.hip_event()) for _ in range(T)]
+    for w in range(T):
+        oa, ra, _, _ = a.step(acts[w])
+        ob, rb, _, _ = b.step(acts[w], evs[w])
+        assert torch.equal(oa, ob) and torch.equal(ra, rb)
+    torch.cuda.synchronize()
+    ms = [nat.hip_event_elapsed_ms(s, e) for s, e in evs]
+    assert all(0.0 < m < 50.0 for m in ms), ms
+    for s, e in evs:
+        nat.hip_event_destroy(s)
+        nat.hip_event_destroy(e)
