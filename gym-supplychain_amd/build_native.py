@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "gym_supplychain_amd", "libscgpu.so")
-SOURCES = ["scg_beergame.hip"]
+SOURCES = ["scg_common.hip", "scg_beergame.hip", "scg_supplychain.hip"]
 ARCH = "gfx950"
 
 
@@ -34,7 +34,7 @@ def build(debug=False, verbose=True):
             print(f"[build_native] {OUT} up to date")
         return OUT
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-fvisibility=hidden", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+           "-fvisibility=hidden", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function",
            "-I", os.path.join(REPO, "include"), "-I", CSRC,
            "-O1" if debug else "-O3", "-o", OUT + ".tmp"] + srcs
     if verbose:

@@ -23,26 +23,11 @@
 #include <cstring>
 #include <vector>
 
+#include "scg_common.h"
 #include "scg_philox.h"
 #include "scgpu.h"
 
 namespace scg {
-
-thread_local char g_err[512] = "";
-
-int fail(int code, const char* fmt, ...) {
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(g_err, sizeof(g_err), fmt, ap);
-  va_end(ap);
-  return code;
-}
-
-int check_launch(const char* what) {
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(SCG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
-  return SCG_OK;
-}
 
 // ---- per-week plan word (host computed, uniform per launch) -------------------------
 enum : int32_t { MODE_DIRECT = 0, MODE_STORE = 1, MODE_ADD = 2, MODE_DROP = 3 };
@@ -488,10 +473,6 @@ using namespace scg;
 
 // ========================================================================================
 extern "C" {
-
-int scg_abi_version(void) { return SCG_ABI_VERSION; }
-
-const char* scg_last_error(void) { return g_err; }
 
 int scg_bg_struct_sizes(size_t* config_size, size_t* state_size) {
   if (config_size) *config_size = sizeof(scg_bg_config);

@@ -1,0 +1,105 @@
+// CPython heapq on fixed-capacity arrays, __host__ __device__.
+//
+// SupplyChainEnv keeps every node's in-transit material as a heapq list of
+// (time, amount) tuples (supplychain_env.py:398-400, pops :222-225) and its observation
+// walks that list in STORAGE order, as if it were sorted (:445-461; SURVEY F9: on the
+// 2-per-stage chain 328 of 360 observations differ from a time-sorted binning). So the
+// storage order is part of the observable state, and this is a restatement of CPython's
+// heappush / heappop / _siftdown / _siftup (Lib/heapq.py, the same algorithm as the C
+// accelerator _heapq.c) over an array, with Python's tuple ordering: compare times, and
+// only when they are equal compare the amounts with NumPy scalar semantics.
+//
+// Layout: entry j of a heap lives at index j*stride of `tk` (time << 3 | NumPy kind) and
+// `val` (amount as double), so env-major strided heaps of many envs can share arrays.
+#pragma once
+
+#include "scg_npscalar.h"
+
+namespace scg {
+
+struct HeapEntry {
+  int32_t tk;  // time << 3 | kind
+  double v;
+};
+
+__host__ __device__ __forceinline__ int32_t he_time(int32_t tk) { return tk >> 3; }
+__host__ __device__ __forceinline__ int he_kind(int32_t tk) { return tk & 7; }
+__host__ __device__ __forceinline__ int32_t he_pack(int32_t time, int kind) { return (time << 3) | kind; }
+
+// Python tuple (t1, a1) < (t2, a2)
+__host__ __device__ __forceinline__ bool he_less(const HeapEntry& x, const HeapEntry& y) {
+  const int32_t tx = he_time(x.tk), ty = he_time(y.tk);
+  if (tx != ty) return tx < ty;
+  const Num ax{x.v, he_kind(x.tk)}, ay{y.v, he_kind(y.tk)};
+  if (np_eq(ax, ay)) return false;
+  return np_lt(ax, ay);
+}
+
+struct HeapView {
+  int32_t* tk;
+  double* val;
+  int64_t stride;
+
+  __host__ __device__ __forceinline__ HeapEntry get(int i) const { return HeapEntry{tk[i * stride], val[i * stride]}; }
+  __host__ __device__ __forceinline__ void put(int i, const HeapEntry& e) const {
+    tk[i * stride] = e.tk;
+    val[i * stride] = e.v;
+  }
+  __host__ __device__ __forceinline__ int32_t time_at(int i) const { return he_time(tk[i * stride]); }
+};
+
+// heapq._siftdown(heap, startpos, pos)
+__host__ __device__ inline void py_siftdown(const HeapView& h, int startpos, int pos) {
+  const HeapEntry item = h.get(pos);
+  while (pos > startpos) {
+    const int parentpos = (pos - 1) >> 1;
+    const HeapEntry parent = h.get(parentpos);
+    if (he_less(item, parent)) {
+      h.put(pos, parent);
+      pos = parentpos;
+      continue;
+    }
+    break;
+  }
+  h.put(pos, item);
+}
+
+// heapq._siftup(heap, pos): move the smaller child up to a leaf, then sift down.
+__host__ __device__ inline void py_siftup(const HeapView& h, int size, int pos) {
+  const int startpos = pos;
+  const HeapEntry item = h.get(pos);
+  int childpos = 2 * pos + 1;
+  while (childpos < size) {
+    const int rightpos = childpos + 1;
+    if (rightpos < size && !he_less(h.get(childpos), h.get(rightpos))) childpos = rightpos;
+    h.put(pos, h.get(childpos));
+    pos = childpos;
+    childpos = 2 * pos + 1;
+  }
+  h.put(pos, item);
+  py_siftdown(h, startpos, pos);
+}
+
+// heapq.heappush. Returns false (and pushes nothing) when the heap is full.
+__host__ __device__ inline bool py_heappush(const HeapView& h, int32_t& size, int cap, const HeapEntry& e) {
+  if (size >= cap) return false;
+  h.put(size, e);
+  ++size;
+  py_siftdown(h, 0, size - 1);
+  return true;
+}
+
+// heapq.heappop on a non-empty heap.
+__host__ __device__ inline HeapEntry py_heappop(const HeapView& h, int32_t& size) {
+  --size;
+  const HeapEntry last = h.get(size);
+  if (size > 0) {
+    const HeapEntry ret = h.get(0);
+    h.put(0, last);
+    py_siftup(h, size, 0);
+    return ret;
+  }
+  return last;
+}
+
+}  // namespace scg

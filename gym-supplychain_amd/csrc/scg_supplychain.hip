@@ -1,0 +1,307 @@
+// SupplyChainEnv hot path for gfx950: reset / step kernels + their C-ABI launchers.
+//
+// Reference: gym_supplychain/envs/supplychain_env.py (snapshot 2024-08-07). One lane owns
+// one env (its whole chain, every node in nodes_info order, as SupplyChainEnv.step walks
+// them, :714-736); the per-env body is scg_supplychain_core.h. State arrays are
+// env-fastest ([slot][N]) so lanes touching the same node/heap slot read one contiguous
+// row; heap positions are data-dependent, so heap traffic is row-gathered through L2.
+// The chain description (scg_sc_node[]) is wave-uniform and read with scalar loads.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "scg_common.h"
+#include "scg_supplychain_core.h"
+#include "scgpu.h"
+
+namespace scg {
+
+constexpr int kScBlock = 64;
+
+struct ScArgs {
+  ScCtx c;
+  double* stock;
+  int32_t* tk;
+  double* val;
+  int32_t* size;
+  const float* act;
+  void* obs;
+  void* term_obs;
+  double* rew;
+  double* ep_ret;
+  double* final_ret;
+  int32_t* err;
+  int64_t n;
+  int64_t env_offset;
+  uint32_t episode;
+  int32_t t;       // the step being simulated (1..T) / 0 for reset
+  int32_t flags;   // bit0 terminal, bit1 autoreset
+  int32_t obs_f64;
+};
+
+struct ObsRow {
+  void* base;
+  int64_t row;
+  int f64;
+  __device__ __forceinline__ void operator()(int o, double x) const {
+    if (f64)
+      static_cast<double*>(base)[row + o] = x;
+    else
+      static_cast<float*>(base)[row + o] = static_cast<float>(x);
+  }
+};
+
+__device__ __forceinline__ ScEnv env_view(const ScArgs& a, int64_t n, uint32_t episode) {
+  return ScEnv{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, static_cast<uint32_t>(a.env_offset + n), episode, 0};
+}
+
+__global__ __launch_bounds__(kScBlock) void sc_reset_kernel(const ScArgs a) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
+  if (n >= a.n) return;
+  ScEnv e = env_view(a, n, a.episode);
+  sc_reset_env(a.c, e);
+  if (a.obs) {
+    ObsRow out{a.obs, n * a.c.O, a.obs_f64};
+    sc_observe(a.c, e, 0, out);
+  }
+  if (a.ep_ret) a.ep_ret[n] = 0.0;
+  if (e.overflow) atomicOr(a.err, 1);
+}
+
+__global__ __launch_bounds__(kScBlock) void sc_step_kernel(const ScArgs a) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
+  if (n >= a.n) return;
+  ScEnv e = env_view(a, n, a.episode);
+  const double reward = sc_step_env(a.c, e, a.act + n * a.c.A, a.t);
+  a.rew[n] = reward;
+  const bool terminal = a.flags & 1;
+  if (a.ep_ret) {
+    const double r = a.ep_ret[n] + reward;  // episode_rewards += current_reward (:739)
+    if (terminal && a.final_ret) a.final_ret[n] = r;
+    a.ep_ret[n] = (a.flags & 2) ? 0.0 : r;
+  }
+  if (a.flags & 2) {  // auto-reset: terminal observation aside, fresh episode in place
+    if (a.term_obs) {
+      ObsRow tout{a.term_obs, n * a.c.O, a.obs_f64};
+      sc_observe(a.c, e, a.t, tout);
+    }
+    e.episode = a.episode + 1;
+    sc_reset_env(a.c, e);
+    ObsRow out{a.obs, n * a.c.O, a.obs_f64};
+    sc_observe(a.c, e, 0, out);
+  } else {
+    ObsRow out{a.obs, n * a.c.O, a.obs_f64};
+    sc_observe(a.c, e, a.t, out);
+    if (terminal && a.term_obs) {
+      ObsRow tout{a.term_obs, n * a.c.O, a.obs_f64};
+      sc_observe(a.c, e, a.t, tout);
+    }
+  }
+  if (e.overflow) atomicOr(a.err, 1);
+}
+
+__global__ __launch_bounds__(kScBlock) void sc_tables_kernel(const ScArgs a, int32_t* __restrict__ demand,
+                                                             int32_t* __restrict__ leadtimes) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
+  if (n >= a.n) return;
+  ScEnv e = env_view(a, n, a.episode);
+  WordCache wc{0, U4{0, 0, 0, 0}, false};
+  const ScCtx& c = a.c;
+  const int64_t per_dem = static_cast<int64_t>(c.T + 1) * c.R * c.P;
+  for (int row = 0; row <= c.T; ++row)
+    for (int r = 0; r < c.R; ++r)
+      for (int p = 0; p < c.P; ++p) demand[n * per_dem + (row * c.R + r) * c.P + p] = sc_demand(c, e, wc, row, r, p);
+  if (leadtimes && c.stochastic) {
+    WordCache lc{0, U4{0, 0, 0, 0}, false};
+    const int64_t per_lt = static_cast<int64_t>(c.T) * c.n_lt;
+    for (int t = 1; t <= c.T; ++t)
+      for (int k = 0; k < c.n_lt; ++k) leadtimes[n * per_lt + (t - 1) * c.n_lt + k] = sc_leadtime(c, e, lc, t, k);
+  }
+}
+
+namespace {
+
+int sc_check(const scg_sc_config* cfg, const scg_sc_state* st) {
+  if (!cfg || !st) return fail(SCG_ERR_INVALID, "null config/state");
+  if (!cfg->nodes || cfg->heap_capacity <= 0 || cfg->n_obs <= 0)
+    return fail(SCG_ERR_INVALID, "config not prepared (call scg_sc_prepare) or no device node table");
+  if (cfg->stochastic_leadtimes && !cfg->leadtime_poisson)
+    return fail(SCG_ERR_INVALID, "stochastic lead times need the Poisson threshold table");
+  if (st->n_envs <= 0) return fail(SCG_ERR_INVALID, "n_envs must be > 0");
+  if (st->env_offset < 0 || st->env_offset + st->n_envs > (int64_t(1) << 32))
+    return fail(SCG_ERR_INVALID, "global env ids must fit in 32 bits");
+  if (!st->stock || !st->heap_tk || !st->heap_val || !st->heap_size || !st->error_flags)
+    return fail(SCG_ERR_INVALID, "state buffers stock/heap_tk/heap_val/heap_size/error_flags are required");
+  return SCG_OK;
+}
+
+ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
+  ScArgs a;
+  std::memset(&a, 0, sizeof(a));
+  ScCtx& c = a.c;
+  c.nodes = cfg->nodes;
+  c.lt_thr = cfg->leadtime_poisson;
+  c.n_nodes = cfg->n_nodes;
+  c.P = cfg->n_products;
+  c.R = cfg->n_retailers;
+  c.A = cfg->n_actions;
+  c.O = cfg->n_obs;
+  c.H = cfg->heap_capacity;
+  c.T = cfg->total_time_steps;
+  c.avg_lt = cfg->avg_leadtime;
+  c.max_lt = cfg->max_leadtime;
+  c.stochastic = cfg->stochastic_leadtimes;
+  c.n_lt = cfg->n_leadtimes;
+  c.lt_thr_len = cfg->leadtime_poisson_len;
+  c.lo = cfg->demand_lo;
+  c.hi = cfg->demand_hi;
+  c.pen_unmet = cfg->unmet_demand_cost;
+  c.pen_stock = cfg->exceeded_stock_capacity_cost;
+  c.pen_proc = cfg->exceeded_process_capacity_cost;
+  c.pen_ship = cfg->exceeded_ship_capacity_cost;
+  c.key0 = static_cast<uint32_t>(st->seed & 0xffffffffu);
+  c.key1 = static_cast<uint32_t>(st->seed >> 32);
+  a.stock = st->stock;
+  a.tk = st->heap_tk;
+  a.val = st->heap_val;
+  a.size = st->heap_size;
+  a.ep_ret = st->episode_return;
+  a.final_ret = st->final_return;
+  a.err = st->error_flags;
+  a.n = st->n_envs;
+  a.env_offset = st->env_offset;
+  a.episode = st->episode;
+  a.obs_f64 = cfg->obs_f64;
+  return a;
+}
+
+dim3 sc_grid(int64_t n) { return dim3(static_cast<unsigned>((n + kScBlock - 1) / kScBlock)); }
+
+}  // namespace
+}  // namespace scg
+
+using namespace scg;
+
+extern "C" {
+
+int scg_sc_struct_sizes(size_t* node_size, size_t* config_size, size_t* state_size) {
+  if (node_size) *node_size = sizeof(scg_sc_node);
+  if (config_size) *config_size = sizeof(scg_sc_config);
+  if (state_size) *state_size = sizeof(scg_sc_state);
+  return SCG_OK;
+}
+
+int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
+  if (!cfg || !nodes) return fail(SCG_ERR_INVALID, "null config/node table");
+  const int NN = cfg->n_nodes, P = cfg->n_products;
+  if (NN < 1 || NN > SCG_SC_MAX_NODES) return fail(SCG_ERR_INVALID, "n_nodes=%d outside 1..%d", NN, SCG_SC_MAX_NODES);
+  if (P < 1 || P > SCG_SC_MAX_PRODUCTS)
+    return fail(SCG_ERR_INVALID, "num_products=%d outside 1..%d", P, SCG_SC_MAX_PRODUCTS);
+  if (cfg->total_time_steps < 1 || cfg->total_time_steps > (1 << 20))
+    return fail(SCG_ERR_INVALID, "total_time_steps=%d out of range", cfg->total_time_steps);
+  if (cfg->avg_leadtime < 1 || cfg->max_leadtime < 1)
+    return fail(SCG_ERR_INVALID, "lead times must be >= 1 (avg %d, max %d)", cfg->avg_leadtime, cfg->max_leadtime);
+  if (cfg->demand_hi <= cfg->demand_lo)
+    return fail(SCG_ERR_INVALID, "demand_range (%d, %d) must have lo < hi", cfg->demand_lo, cfg->demand_hi);
+  int n_act = 0, n_lt = 0, n_ret = 0;
+  for (int i = 0; i < NN; ++i) {
+    const scg_sc_node& nd = nodes[i];
+    if (nd.action_offset != n_act) return fail(SCG_ERR_INVALID, "node %d: action_offset %d != %d", i, nd.action_offset, n_act);
+    if (cfg->stochastic_leadtimes && nd.leadtime_offset != n_lt)
+      return fail(SCG_ERR_INVALID, "node %d: leadtime_offset %d != %d", i, nd.leadtime_offset, n_lt);
+    if (nd.n_dests < 0 || nd.n_dests > SCG_SC_MAX_DESTS)
+      return fail(SCG_ERR_INVALID, "node %d: %d destinations (max %d)", i, nd.n_dests, SCG_SC_MAX_DESTS);
+    if (!nd.last_level && nd.n_dests == 0) return fail(SCG_ERR_INVALID, "node %d ships but has no destinations", i);
+    for (int d = 0; d < nd.n_dests; ++d)
+      if (nd.dests[d] < 0 || nd.dests[d] >= NN) return fail(SCG_ERR_INVALID, "node %d: bad destination", i);
+    for (int p = 0; p < P; ++p) {
+      if (nd.n_init[p] < 0 || nd.n_init[p] > SCG_SC_MAX_INIT)
+        return fail(SCG_ERR_INVALID, "node %d: %d initial pipeline entries (max %d)", i, nd.n_init[p], SCG_SC_MAX_INIT);
+      if (nd.stock_capacity[p] <= 0) return fail(SCG_ERR_INVALID, "node %d: stock_capacity must be > 0", i);
+      if (nd.processing_capacity > 0 && nd.processing_ratio[p] == 0)
+        return fail(SCG_ERR_INVALID, "node %d: processing node with zero processing ratio", i);
+    }
+    if (nd.last_level) {
+      if (nd.retailer_index != n_ret) return fail(SCG_ERR_INVALID, "node %d: retailer_index", i);
+      ++n_ret;
+    }
+    n_act += nd.n_supply + nd.n_ship;
+    n_lt += (nd.n_supply > 0 ? P : 0) + nd.n_dests;
+  }
+  if (n_ret != cfg->n_retailers || n_ret < 1) return fail(SCG_ERR_INVALID, "retailer count mismatch");
+  // heap bound: pushes per step into (node, p) x (longest lead time + 1) + initial entries
+  std::vector<int> indeg(static_cast<size_t>(NN) * P, 0);
+  for (int i = 0; i < NN; ++i) {
+    const scg_sc_node& nd = nodes[i];
+    for (int p = 0; p < P; ++p) {
+      if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) indeg[i * P + p] += 1;
+      if (!nd.last_level)
+        for (int d = 0; d < nd.n_dests; ++d) indeg[nd.dests[d] * P + p] += 1;
+    }
+  }
+  const int lmax = cfg->stochastic_leadtimes ? cfg->max_leadtime : cfg->avg_leadtime;
+  int H = 1;
+  for (int i = 0; i < NN; ++i)
+    for (int p = 0; p < P; ++p) H = std::max(H, indeg[i * P + p] * (lmax + 1) + nodes[i].n_init[p]);
+  cfg->n_actions = n_act;
+  cfg->n_leadtimes = n_lt;
+  cfg->n_obs = n_ret * P + NN * P + NN * P * cfg->avg_leadtime + 1;
+  cfg->heap_capacity = H;
+  return SCG_OK;
+}
+
+int scg_sc_reset(const scg_sc_config* cfg, scg_sc_state* st, void* obs, void* stream) {
+  if (int rc = sc_check(cfg, st)) return rc;
+  if (st->time_step >= 0) st->episode += 1;
+  ScArgs a = sc_args(cfg, st);
+  a.obs = obs;
+  hipLaunchKernelGGL(sc_reset_kernel, sc_grid(st->n_envs), dim3(kScBlock), 0, static_cast<hipStream_t>(stream), a);
+  if (int rc = check_launch("sc_reset_kernel")) return rc;
+  st->time_step = 0;
+  return SCG_OK;
+}
+
+int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action, void* obs, double* reward,
+                void* terminal_obs, uint32_t flags, int32_t* done, void* stream) {
+  if (int rc = sc_check(cfg, st)) return rc;
+  if (!action || !obs || !reward) return fail(SCG_ERR_INVALID, "action/obs/reward buffers are required");
+  if (st->time_step < 0) return fail(SCG_ERR_NOT_RESET, "step() before reset()");
+  const int T = cfg->total_time_steps;
+  if (st->time_step >= T) return fail(SCG_ERR_PAST_HORIZON, "step() after the terminal step %d", T);
+  const int t = st->time_step + 1;
+  const bool terminal = t == T;
+  const bool autoreset = terminal && (flags & SCG_BG_AUTORESET);
+  ScArgs a = sc_args(cfg, st);
+  a.act = action;
+  a.obs = obs;
+  a.term_obs = terminal_obs;
+  a.rew = reward;
+  a.t = t;
+  a.flags = (terminal ? 1 : 0) | (autoreset ? 2 : 0);
+  hipLaunchKernelGGL(sc_step_kernel, sc_grid(st->n_envs), dim3(kScBlock), 0, static_cast<hipStream_t>(stream), a);
+  if (int rc = check_launch("sc_step_kernel")) return rc;
+  if (autoreset) {
+    st->time_step = 0;
+    st->episode += 1;
+  } else {
+    st->time_step = t;
+  }
+  if (done) *done = terminal ? 1 : 0;
+  return SCG_OK;
+}
+
+int scg_sc_draw_tables(const scg_sc_config* cfg, const scg_sc_state* st, uint32_t episode, int32_t* demand,
+                       int32_t* leadtimes, void* stream) {
+  if (int rc = sc_check(cfg, st)) return rc;
+  if (!demand) return fail(SCG_ERR_INVALID, "null demand buffer");
+  ScArgs a = sc_args(cfg, st);
+  a.episode = episode;
+  hipLaunchKernelGGL(sc_tables_kernel, sc_grid(st->n_envs), dim3(kScBlock), 0, static_cast<hipStream_t>(stream), a,
+                     demand, leadtimes);
+  return check_launch("sc_tables_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,317 @@
+// SupplyChainEnv step / reset / observation for ONE env, __host__ __device__.
+//
+// Restates supplychain_env.py (snapshot 2024-08-07): SC_Node.act (:208-396) with
+// SC_Action.apply (:42-98), the heapq pipeline (:398-400), SC_Node.reset (:402-412),
+// SC_Node.build_observation (:428-463) and SupplyChainEnv.step/_build_observation
+// (:703-791). Every scalar is a scg::Num carrying its NumPy kind (scg_npscalar.h) so the
+// float32/float64 rounding of the reference is reproduced; heaps follow CPython's heapq
+// (scg_pyheap.h). The kernel (scg_supplychain.hip) runs one env per lane with these
+// functions over env-fastest SoA arrays.
+#pragma once
+
+#include <stdint.h>
+
+#include "scg_npscalar.h"
+#include "scg_philox.h"
+#include "scg_pyheap.h"
+#include "scgpu.h"
+
+namespace scg {
+
+// Launch-uniform view of the configuration.
+struct ScCtx {
+  const scg_sc_node* nodes;
+  const uint32_t* lt_thr;
+  int32_t n_nodes, P, R, A, O, H, T;
+  int32_t avg_lt, max_lt, stochastic, n_lt, lt_thr_len;
+  int32_t lo, hi;
+  int32_t pen_unmet, pen_stock, pen_proc, pen_ship;
+  uint32_t key0, key1;
+};
+
+// One env's state: element i of a per-env array lives at [i * stride].
+struct ScEnv {
+  double* stock;     // [NP]
+  int32_t* tk;       // [NP][H]
+  double* val;       // [NP][H]
+  int32_t* size;     // [NP]
+  int64_t stride;    // envs in the batch
+  uint32_t env_id;   // global id (Philox counter)
+  uint32_t episode;
+  int32_t overflow;  // set when a push met a full heap (the push is dropped)
+};
+
+__host__ __device__ __forceinline__ HeapView sc_heap(const ScCtx& c, const ScEnv& e, int node, int p) {
+  const int64_t hp = static_cast<int64_t>(node) * c.P + p;
+  return HeapView{e.tk + hp * c.H * e.stride, e.val + hp * c.H * e.stride, e.stride};
+}
+
+__host__ __device__ __forceinline__ int32_t& sc_size(const ScCtx& c, const ScEnv& e, int node, int p) {
+  return e.size[(static_cast<int64_t>(node) * c.P + p) * e.stride];
+}
+
+__host__ __device__ __forceinline__ double& sc_stock(const ScCtx& c, const ScEnv& e, int node, int p) {
+  return e.stock[(static_cast<int64_t>(node) * c.P + p) * e.stride];
+}
+
+// Philox word cache: consecutive words of one (env, episode, stream) come 4 per call.
+struct WordCache {
+  uint32_t blk;
+  U4 w;
+  bool valid;
+};
+
+__host__ __device__ __forceinline__ uint32_t cached_word(const ScCtx& c, const ScEnv& e, WordCache& wc, uint32_t j,
+                                                         uint32_t stream) {
+  const uint32_t blk = j >> 2;
+  if (!wc.valid || wc.blk != blk) {
+    wc.w = philox4x32_10(U4{e.env_id, e.episode, blk, stream}, c.key0, c.key1);
+    wc.blk = blk;
+    wc.valid = true;
+  }
+  const uint32_t s = j & 3u;
+  return s == 0 ? wc.w.x : s == 1 ? wc.w.y : s == 2 ? wc.w.z : wc.w.w;
+}
+
+// customer_demands[row, r, p] (np.int64): uniform integer in [lo, hi]
+__host__ __device__ __forceinline__ int32_t sc_demand(const ScCtx& c, const ScEnv& e, WordCache& wc, int row, int r,
+                                                      int p) {
+  const uint32_t j = static_cast<uint32_t>((row * c.R + r) * c.P + p);
+  const uint32_t u = cached_word(c, e, wc, j, SCG_STREAM_SC_DEMAND);
+  const uint64_t span = static_cast<uint64_t>(c.hi - c.lo + 1);
+  return c.lo + static_cast<int32_t>((static_cast<uint64_t>(u) * span) >> 32);
+}
+
+// leadtimes[t-1, k]: clip(1 + Poisson(avg-1), 1, max)   (:670-672)
+__host__ __device__ __forceinline__ int32_t sc_leadtime(const ScCtx& c, const ScEnv& e, WordCache& wc, int t, int k) {
+  const uint32_t j = static_cast<uint32_t>((t - 1) * c.n_lt + k);
+  const uint32_t u = cached_word(c, e, wc, j, SCG_STREAM_SC_LEADTIME);
+  int32_t x = 0;
+  for (int i = 0; i < c.lt_thr_len; ++i) x += (c.lt_thr[i] <= u) ? 1 : 0;
+  x += 1;
+  return x < 1 ? 1 : (x > c.max_lt ? c.max_lt : x);
+}
+
+// Lead time #i of a node in step t (deterministic: avg_leadtime for every action, :724).
+__host__ __device__ __forceinline__ int32_t node_leadtime(const ScCtx& c, const ScEnv& e, WordCache& wc,
+                                                          const scg_sc_node& nd, int t, int i) {
+  if (!c.stochastic) return c.avg_lt;
+  return sc_leadtime(c, e, wc, t, nd.leadtime_offset + i);
+}
+
+__host__ __device__ __forceinline__ void sc_push(const ScCtx& c, ScEnv& e, int node, int p, int32_t time, Num amount) {
+  int32_t& sz = sc_size(c, e, node, p);
+  if (!py_heappush(sc_heap(c, e, node, p), sz, c.H, HeapEntry{he_pack(time, amount.k), amount.v})) e.overflow = 1;
+}
+
+// SC_Node.reset (:402-412): stock back to initial_stock, heaps re-seeded at times 1..k
+// (initial_supply entries first, then initial_shipments, each pushed with heappush).
+__host__ __device__ inline void sc_reset_env(const ScCtx& c, ScEnv& e) {
+  for (int i = 0; i < c.n_nodes; ++i) {
+    const scg_sc_node& nd = c.nodes[i];
+    for (int p = 0; p < c.P; ++p) {
+      sc_stock(c, e, i, p) = static_cast<double>(nd.initial_stock[p]);
+      sc_size(c, e, i, p) = 0;
+      for (int j = 0; j < nd.n_init[p]; ++j) sc_push(c, e, i, p, nd.init_time[p][j], pyint(nd.init_amount[p][j]));
+    }
+  }
+}
+
+// SC_Action.apply for SHIP (:58-96): the cut [0, limit] split at the destinations'
+// sorted action values; amount_i = (v_(k) - v_(k-1)) * limit, clamped to what is left.
+__host__ __device__ inline void sc_split(const Num* vals, int D, Num limit, Num* out) {
+  for (int i = 0; i < D; ++i) out[i] = pyint(0);
+  Num left = limit;
+  if (!np_lt(pyint(0), left)) return;
+  int order[SCG_SC_MAX_DESTS];
+  for (int i = 0; i < D; ++i) {  // stable insertion sort on (value, index)
+    int j = i;
+    while (j > 0 && np_lt(vals[i], vals[order[j - 1]])) {
+      order[j] = order[j - 1];
+      --j;
+    }
+    order[j] = i;
+  }
+  Num prev = pyint(0);
+  for (int s = 0; s < D; ++s) {
+    const int i = order[s];
+    Num amt = np_mul(np_sub(vals[i], prev), limit);
+    if (np_lt(left, amt)) amt = left;
+    out[i] = amt;
+    left = np_sub(left, amt);
+    prev = vals[i];
+  }
+}
+
+// Action k of this env, denormalised like _denormalize_action (:697-698): (a + 1) / 2 on
+// a float32 array stays float32.
+__host__ __device__ __forceinline__ Num sc_action(const float* raw, int k) {
+  return Num{static_cast<double>((raw[k] + 1.0f) / 2.0f), NK_F32};
+}
+
+// SC_Node.act (:208-396) for node `ni` at time t; `act` = this env's raw float32 action
+// row. Returns the node's cost with its NumPy kind.
+__host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& ltc, WordCache& dmc, int ni,
+                                           const float* act, int t) {
+  const scg_sc_node& nd = c.nodes[ni];
+  const int P = c.P;
+  Num cost = pyint(0);
+  int lt_i = 0;
+  // receive (:220-228): pop every entry due now, summed in a float64 array
+  for (int p = 0; p < P; ++p) {
+    const HeapView h = sc_heap(c, e, ni, p);
+    int32_t& sz = sc_size(c, e, ni, p);
+    double recv = 0.0;
+    while (sz > 0 && h.time_at(0) == t) recv = recv + py_heappop(h, sz).v;
+    sc_stock(c, e, ni, p) = sc_stock(c, e, ni, p) + recv;
+  }
+  // over stock capacity: penalty, excess discarded (:232-240)
+  for (int p = 0; p < P; ++p) {
+    double& st = sc_stock(c, e, ni, p);
+    if (st > static_cast<double>(nd.stock_capacity[p])) {
+      cost = np_add(cost, np_mul(pyint(c.pen_stock), np_sub(f64(st), pyint(nd.stock_capacity[p]))));
+      st = static_cast<double>(nd.stock_capacity[p]);
+    }
+  }
+  // SUPPLY (:243-259)
+  int a_i = 0;
+  if (nd.n_supply > 0) {
+    for (int p = 0; p < P; ++p) {
+      if (nd.supply_capacity[p] <= 0) continue;
+      const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));
+      const Num cst = np_mul(amount, pyint(nd.supply_cost[p]));
+      ++a_i;
+      if (np_lt(pyint(0), amount)) {
+        sc_push(c, e, ni, p, t + node_leadtime(c, e, ltc, nd, t, lt_i), amount);
+        ++lt_i;  // the lead-time cursor moves only when something was supplied (:252-254)
+      }
+      cost = np_add(cost, cst);
+    }
+  }
+  if (!nd.last_level) {
+    // SHIP (:262-375)
+    const int D = nd.n_dests;
+    Num ship_left[SCG_SC_MAX_DESTS];
+    for (int i = 0; i < D; ++i) ship_left[i] = pyint(nd.ship_capacity[i]);
+    Num proc_left = pyint(nd.processing_capacity);
+    const int lt_base = lt_i;
+    for (int p = 0; p < P; ++p) {
+      if (!(nd.stock_capacity[p] > 0)) continue;  // no SHIP action for this product
+      Num over_ship = pyint(0), over_proc = pyint(0);
+      const Num material = f64(sc_stock(c, e, ni, p));
+      if (np_lt(pyint(0), material)) {
+        Num vals[SCG_SC_MAX_DESTS], out[SCG_SC_MAX_DESTS], sent[SCG_SC_MAX_DESTS];
+        for (int i = 0; i < D; ++i) vals[i] = sc_action(act, nd.action_offset + a_i + i);
+        sc_split(vals, D, py_min(pyint(nd.stock_capacity[p]), material), out);
+        for (int i = 0; i < D; ++i) sent[i] = out[i];
+        if (nd.processing_capacity > 0) {  // factory: processing capacity and ratio (:298-310)
+          for (int i = 0; i < D; ++i) {
+            if (np_lt(pyint(0), out[i])) {
+              if (np_lt(proc_left, out[i])) {
+                over_proc = np_add(over_proc, np_sub(out[i], proc_left));
+                out[i] = proc_left;
+              }
+              proc_left = np_sub(proc_left, out[i]);
+            }
+            sent[i] = np_div(out[i], pyint(nd.processing_ratio[p]));
+          }
+        }
+        for (int i = 0; i < D; ++i) {  // per-destination ship capacity (:312-328)
+          const Num amt = sent[i];
+          if (np_lt(pyint(0), amt) && np_lt(ship_left[i], amt)) {
+            over_ship = np_add(over_ship, np_sub(amt, ship_left[i]));
+            sent[i] = ship_left[i];
+            out[i] = nd.processing_capacity > 0 ? np_mul(sent[i], pyint(nd.processing_ratio[p])) : sent[i];
+            ship_left[i] = np_sub(ship_left[i], out[i]);  // only on overflow, by out[i]
+          }
+        }
+        Num leaving = pyint(0);  // sum(amounts) (:331)
+        for (int i = 0; i < D; ++i) leaving = np_add(leaving, out[i]);
+        double& st = sc_stock(c, e, ni, p);
+        st = st - leaving.v;  // float64 array element minus the promoted scalar (:332)
+        if (nd.processing_capacity > 0) cost = np_add(cost, np_mul(leaving, pyint(nd.processing_cost[p])));
+        int lt_k = lt_base;
+        for (int i = 0; i < D; ++i) {  // (:344-348)
+          if (np_lt(pyint(0), sent[i])) sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_k), sent[i]);
+          ++lt_k;
+        }
+        Num ship_cost = pyint(0);  // sum(calculate_costs(amounts_to_ship)) (:352)
+        for (int i = 0; i < D; ++i) ship_cost = np_add(ship_cost, np_mul(sent[i], pyint(nd.dest_costs[p][i])));
+        cost = np_add(cost, ship_cost);
+      }
+      cost = np_add(cost, np_mul(pyint(c.pen_proc), over_proc));  // :361
+      cost = np_add(cost, np_mul(pyint(c.pen_ship), over_ship));  // :366
+      a_i += D;
+    }
+  } else {
+    // retailer: serve what stock allows, lost sales cost the rest (:379-387)
+    for (int p = 0; p < P; ++p) {
+      const Num dem = Num{static_cast<double>(sc_demand(c, e, dmc, t - 1, nd.retailer_index, p)), NK_I64};
+      double& st = sc_stock(c, e, ni, p);
+      const Num served = py_min(f64(st), dem);
+      st = st - served.v;
+      cost = np_add(cost, np_mul(pyint(c.pen_unmet), np_sub(dem, served)));
+    }
+  }
+  for (int p = 0; p < P; ++p)  // holding (:390-394)
+    cost = np_add(cost, np_mul(f64(sc_stock(c, e, ni, p)), pyint(nd.stock_cost[p])));
+  return cost;
+}
+
+// SupplyChainEnv.step body (:704-738) for time t (already incremented). Actions are the
+// raw float32 row in [-1, 1]; returns the reward.
+__host__ __device__ inline double sc_step_env(const ScCtx& c, ScEnv& e, const float* act, int t) {
+  WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
+  Num total = pyint(0);
+  for (int i = 0; i < c.n_nodes; ++i) total = np_add(total, sc_node_act(c, e, ltc, dmc, i, act, t));
+  return np_neg(total).v;
+}
+
+// Observation at time t (:762-791): normalised next demands, per node stock share and
+// in-transit bins (storage-order walk, :445-461), time to go; 2x-1 clipped to [-1, 1].
+template <class Sink>
+__host__ __device__ inline void sc_observe(const ScCtx& c, ScEnv& e, int t, Sink& out) {
+  int o = 0;
+  WordCache dmc{0, U4{0, 0, 0, 0}, false};
+  auto emit = [&](double x) {
+    double y = x * 2.0 - 1.0;
+    y = y < -1.0 ? -1.0 : (y > 1.0 ? 1.0 : y);
+    out(o++, y);
+  };
+  const double range = static_cast<double>(c.hi - c.lo);
+  for (int r = 0; r < c.R; ++r)
+    for (int p = 0; p < c.P; ++p) emit(static_cast<double>(sc_demand(c, e, dmc, t, r, p) - c.lo) / range);
+  const int first = t + 1, last = t + c.avg_lt;
+  for (int i = 0; i < c.n_nodes; ++i) {
+    const scg_sc_node& nd = c.nodes[i];
+    for (int p = 0; p < c.P; ++p) emit(sc_stock(c, e, i, p) / static_cast<double>(nd.stock_capacity[p]));
+    for (int p = 0; p < c.P; ++p) {
+      const HeapView h = sc_heap(c, e, i, p);
+      const int32_t sz = sc_size(c, e, i, p);
+      if (sz == 0) {
+        for (int b = first; b <= last; ++b) emit(0.0);
+        continue;
+      }
+      int k = 0;
+      for (int when = first; when < last; ++when) {
+        Num bin = pyint(0);
+        while (k < sz && h.time_at(k) == when) {
+          const HeapEntry en = h.get(k);
+          bin = np_add(bin, Num{en.v, he_kind(en.tk)});
+          ++k;
+        }
+        emit(np_div(bin, pyint(nd.max_ship[p])).v);
+      }
+      Num bin = pyint(0);
+      while (k < sz) {
+        const HeapEntry en = h.get(k);
+        bin = np_add(bin, Num{en.v, he_kind(en.tk)});
+        ++k;
+      }
+      emit(np_div(bin, pyint(nd.max_ship[p] * (c.max_lt - (last - first)))).v);
+    }
+  }
+  emit(static_cast<double>(c.T - t) / static_cast<double>(c.T));
+}
+
+}  // namespace scg

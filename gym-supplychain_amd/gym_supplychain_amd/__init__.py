@@ -9,16 +9,43 @@ dynamics run as fused HIP kernels through the C ABI in include/scgpu.h.
     venv = gsa.make_vec("beergame-v0", 65536, demand="poisson", seed=0)   # batched
 """
 from . import _native  # noqa: F401  (fails loudly when libscgpu.so is missing)
-from .envs import BeerGameEnv, BeerGameVecEnv
+from .envs import (SCENARIOS, BeerGameEnv, BeerGameVecEnv, SupplyChain2perStageEnv, SupplyChainEnv,
+                   SupplyChainMultiProduct, SupplyChainMultiProduct_IncreasingCosts, SupplyChainNPerStage,
+                   SupplyChainVecEnv)
 
-__all__ = ["BeerGameEnv", "BeerGameVecEnv", "ENV_IDS", "VEC_ENV_IDS", "make", "make_vec", "register_gym"]
+__all__ = ["BeerGameEnv", "BeerGameVecEnv", "SupplyChainEnv", "SupplyChainVecEnv", "SupplyChain2perStageEnv",
+           "SupplyChainNPerStage", "SupplyChainMultiProduct", "SupplyChainMultiProduct_IncreasingCosts",
+           "ENV_IDS", "VEC_ENV_IDS", "make", "make_vec", "register_gym"]
 
-# id -> entry point, as registered by the reference (gym_supplychain/__init__.py:3-6)
+# id -> entry point, as registered by the reference (gym_supplychain/__init__.py:3-51).
+# Ids whose demand model is not on the GPU path yet (seasonal / per-product demand
+# configs: beergame-v2, sc-2perstage-seasonal-v0, sc-2perstage-multiproduct-v1,
+# sc-2perstage-multiproduct-inccosts-v1) are not registered.
 ENV_IDS = {
     "beergame-v0": "gym_supplychain_amd.envs:BeerGameEnv",
+    "supplychain-v0": "gym_supplychain_amd.envs:SupplyChainEnv",
+    "sc-2perstage-v0": "gym_supplychain_amd.envs:SupplyChain2perStageEnv",
+    "sc-2perstage-multiproduct-v0": "gym_supplychain_amd.envs:SupplyChainMultiProduct",
+    "sc-Nperstage-multiproduct-v0": "gym_supplychain_amd.envs:SupplyChainNPerStage",
+    "sc-2perstage-multiproduct-inccosts-v0": "gym_supplychain_amd.envs:SupplyChainMultiProduct_IncreasingCosts",
 }
+_VEC_KEYS = ("seed", "device", "env_offset", "auto_reset", "obs_dtype", "track_returns")
+
+
+def _sc_vec(builder):
+    def make(n_envs, **kw):
+        vec_kw = {k: kw.pop(k) for k in _VEC_KEYS if k in kw}
+        nodes, env_kw = builder(**kw)
+        seed = env_kw.pop("seed", None)
+        vec_kw.setdefault("seed", seed if seed is not None else 0)
+        return SupplyChainVecEnv(n_envs, nodes, **vec_kw, **env_kw)
+    return make
+
+
 VEC_ENV_IDS = {
     "beergame-v0": BeerGameVecEnv,
+    "supplychain-v0": SupplyChainVecEnv,
+    **{env_id: _sc_vec(b) for env_id, b in SCENARIOS.items()},
 }
 
 

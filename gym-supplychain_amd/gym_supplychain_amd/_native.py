@@ -85,6 +85,50 @@ class BgState(ctypes.Structure):
     ]
 
 
+SC_MAX_PRODUCTS = 8
+SC_MAX_DESTS = 32
+SC_MAX_INIT = 16
+SC_MAX_NODES = 256
+SCG_STREAM_SC_DEMAND = 2
+SCG_STREAM_SC_LEADTIME = 3
+
+_PA = ctypes.c_int32 * SC_MAX_PRODUCTS
+
+
+class ScNode(ctypes.Structure):
+    """scg_sc_node (include/scgpu.h)."""
+    _fields_ = [
+        ("last_level", ctypes.c_int32), ("n_supply", ctypes.c_int32), ("n_ship", ctypes.c_int32),
+        ("n_dests", ctypes.c_int32), ("processing_capacity", ctypes.c_int32), ("retailer_index", ctypes.c_int32),
+        ("action_offset", ctypes.c_int32), ("leadtime_offset", ctypes.c_int32),
+        ("supply_capacity", _PA), ("supply_cost", _PA), ("stock_capacity", _PA), ("stock_cost", _PA),
+        ("processing_ratio", _PA), ("processing_cost", _PA), ("max_ship", _PA), ("initial_stock", _PA),
+        ("n_init", _PA),
+        ("init_time", (ctypes.c_int32 * SC_MAX_INIT) * SC_MAX_PRODUCTS),
+        ("init_amount", (ctypes.c_int32 * SC_MAX_INIT) * SC_MAX_PRODUCTS),
+        ("dests", ctypes.c_int32 * SC_MAX_DESTS), ("ship_capacity", ctypes.c_int32 * SC_MAX_DESTS),
+        ("dest_costs", (ctypes.c_int32 * SC_MAX_DESTS) * SC_MAX_PRODUCTS),
+    ]
+
+
+class ScConfig(ctypes.Structure):
+    """scg_sc_config (include/scgpu.h)."""
+    _fields_ = [(f, ctypes.c_int32) for f in (
+        "n_nodes", "n_products", "n_retailers", "n_actions", "n_obs", "n_leadtimes", "total_time_steps",
+        "avg_leadtime", "max_leadtime", "stochastic_leadtimes", "demand_lo", "demand_hi", "unmet_demand_cost",
+        "exceeded_stock_capacity_cost", "exceeded_process_capacity_cost", "exceeded_ship_capacity_cost",
+        "heap_capacity", "leadtime_poisson_len", "obs_f64", "reserved")] + [
+        ("nodes", ctypes.c_void_p), ("leadtime_poisson", ctypes.c_void_p)]
+
+
+class ScState(ctypes.Structure):
+    """scg_sc_state (include/scgpu.h)."""
+    _fields_ = [("n_envs", ctypes.c_int64), ("env_offset", ctypes.c_int64), ("seed", ctypes.c_uint64),
+                ("episode", ctypes.c_uint32), ("time_step", ctypes.c_int32)] + [
+        (f, ctypes.c_void_p) for f in ("stock", "heap_tk", "heap_val", "heap_size", "episode_return",
+                                       "final_return", "error_flags")]
+
+
 # Every symbol include/scgpu.h declares, with its ctypes signature.
 SIGNATURES = {
     "scg_abi_version": (ctypes.c_int, []),
@@ -105,6 +149,15 @@ SIGNATURES = {
                                       ctypes.c_void_p]),
     "scg_bg_poisson_demand": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState),
                                              ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "scg_sc_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t)] * 3),
+    "scg_sc_prepare": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScNode)]),
+    "scg_sc_reset": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.c_void_p,
+                                    ctypes.c_void_p]),
+    "scg_sc_step": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, _i32p,
+                                   ctypes.c_void_p]),
+    "scg_sc_draw_tables": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.c_uint32,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "scg_uniform_ints": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                         ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_void_p, ctypes.c_void_p]),
@@ -132,6 +185,11 @@ def _load():
     if (cs.value, ss.value) != (ctypes.sizeof(BgConfig), ctypes.sizeof(BgState)):
         raise NativeLibraryError(f"struct layout mismatch: C ({cs.value}, {ss.value}) vs ctypes "
                                  f"({ctypes.sizeof(BgConfig)}, {ctypes.sizeof(BgState)})")
+    ns, cs, ss = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    lib.scg_sc_struct_sizes(ctypes.byref(ns), ctypes.byref(cs), ctypes.byref(ss))
+    want = (ctypes.sizeof(ScNode), ctypes.sizeof(ScConfig), ctypes.sizeof(ScState))
+    if (ns.value, cs.value, ss.value) != want:
+        raise NativeLibraryError(f"SupplyChain struct layout mismatch: C {(ns.value, cs.value, ss.value)} vs {want}")
     return lib
 
 

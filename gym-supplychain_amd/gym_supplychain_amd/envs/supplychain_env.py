@@ -1,0 +1,476 @@
+"""Generic multi-echelon supply chain on MI355X: ``SupplyChainVecEnv`` and the drop-in
+``SupplyChainEnv`` plus the reference's scenario classes.
+
+Mirrors gym_supplychain.envs.SupplyChainEnv (gym_supplychain/envs/supplychain_env.py,
+snapshot 2024-08-07): same nodes_info schema and constructor keywords (:482-628), same
+reset()/step() results (:630-748). The dynamics — SC_Node.act with SC_Action.apply, the
+heapq in-transit pipeline, the observation walk over heap storage order — run in
+gym-supplychain_amd/csrc/scg_supplychain.hip through include/scgpu.h; this module
+resolves the configuration into the flat node table the kernels read and owns the
+device buffers.
+
+Differences from the reference:
+  * per-episode demand and stochastic lead times are drawn on device with Philox (same
+    distributions: uniform randint demand, clip(1 + Poisson(avg-1), 1, max) lead times)
+    instead of MT19937 RandomState, keyed by `seed` and the global env id;
+  * actions are float32 (the declared Box dtype); the vec env's observations are float32
+    by default (float64, the reference's dtype, on request and in the single-env class);
+  * normal / sinusoidal demand, demand_config_by_product and build_info are not yet
+    supported and raise NotImplementedError.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from .. import _native as nat
+from .. import spaces
+
+_MAXP = nat.SC_MAX_PRODUCTS
+_MAXD = nat.SC_MAX_DESTS
+_MAXI = nat.SC_MAX_INIT
+
+
+def _per_product(value, P, what):
+    """SC_Node._treat_int_or_list_param (:178-191)."""
+    if type(value) is list:
+        if len(value) == 0:
+            return [0] * P
+        if len(value) != P:
+            raise AssertionError(f"{what}: expected one value per product ({P}), got {len(value)}")
+        return list(value)
+    if type(value) is int:
+        return [value] * P
+    raise ValueError(f"Invalid param: '{value}' should be an int or a list with one value per product")
+
+
+def _int(name, v):
+    if isinstance(v, (bool, np.bool_)) or not isinstance(v, (int, np.integer)):
+        raise TypeError(f"{name} must be an integer (got {v!r}); the GPU path keeps the reference's int costs")
+    v = int(v)
+    if abs(v) >= 2 ** 31:
+        raise ValueError(f"{name}={v} does not fit int32")
+    return v
+
+
+class SupplyChainSpec:
+    """SupplyChainEnv.__init__ (:482-628) resolved into scg_sc_node records."""
+
+    def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
+                 exceeded_process_capacity_cost=1000, exceeded_ship_capacity_cost=1000,
+                 demand_config_by_product=False, demand_range=(10, 20), demand_std=None, demand_sen_peaks=None,
+                 avg_demand_range=None, processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2,
+                 max_leadtime=2, total_time_steps=360, seed=None, build_info=False, demand_perturb_norm=False):
+        if demand_config_by_product:
+            raise NotImplementedError("demand_config_by_product=True is not supported on the GPU path yet")
+        if demand_std is not None or demand_sen_peaks is not None:
+            raise NotImplementedError("only uniform demand (demand_std=None, demand_sen_peaks=None) is supported yet")
+        if build_info:
+            raise NotImplementedError("build_info ledgers are not supported on the GPU path yet")
+        P = _int("num_products", num_products)
+        if not 1 <= P <= _MAXP:
+            raise ValueError(f"num_products={P} outside 1..{_MAXP}")
+        lo, hi = demand_range
+        if lo == hi:
+            raise AssertionError("demand_range must not be empty")  # :592
+        self.P = P
+        self.demand_range = (_int("demand_range[0]", lo), _int("demand_range[1]", hi))
+        if self.demand_range[1] < self.demand_range[0]:
+            raise ValueError("demand_range must be (low, high) with low < high")
+        self.penalties = dict(unmet_demand_cost=_int("unmet_demand_cost", unmet_demand_cost),
+                              exceeded_stock_capacity_cost=_int("exceeded_stock_capacity_cost",
+                                                                exceeded_stock_capacity_cost),
+                              exceeded_process_capacity_cost=_int("exceeded_process_capacity_cost",
+                                                                  exceeded_process_capacity_cost),
+                              exceeded_ship_capacity_cost=_int("exceeded_ship_capacity_cost",
+                                                               exceeded_ship_capacity_cost))
+        self.stochastic_leadtimes = bool(stochastic_leadtimes)
+        self.avg_leadtime = _int("avg_leadtime", avg_leadtime)
+        self.max_leadtime = _int("max_leadtime", max_leadtime)
+        self.total_time_steps = _int("total_time_steps", total_time_steps)
+        self.seed = seed
+        self.processing_ratio = processing_ratio
+        names = list(nodes_info)
+        if not 1 <= len(names) <= nat.SC_MAX_NODES:
+            raise ValueError(f"{len(names)} nodes (1..{nat.SC_MAX_NODES} supported)")
+        index = {n: i for i, n in enumerate(names)}
+        self.node_names = names
+        nodes = []
+        for name in names:
+            info = nodes_info[name]
+            proc_cost = info.get("processing_cost", 0)
+            no_proc = ((type(proc_cost) is int and proc_cost == 0) or
+                       (type(proc_cost) is list and sum(proc_cost) == 0))           # :518-522
+            supply_cap = _per_product(info.get("supply_capacity", 0), P, "supply_capacity")
+            nd = dict(
+                name=name,
+                last_level=bool(info.get("last_level", False)),
+                ratio=_per_product(0 if no_proc else processing_ratio, P, "processing_ratio"),
+                processing_cost=_per_product(proc_cost, P, "processing_cost"),
+                processing_capacity=info.get("processing_capacity", 0),
+                supply_capacity=supply_cap if max(supply_cap) > 0 else [0] * P,
+                supply_cost=_per_product(info.get("supply_cost", 0), P, "supply_cost"),
+                max_ship=list(supply_cap) if max(supply_cap) > 0 else [0] * P,
+                initial_stock=_per_product(info.get("initial_stock", 0), P, "initial_stock"),
+                stock_capacity=_per_product(info.get("stock_capacity", float("inf")), P, "stock_capacity"),
+                stock_cost=_per_product(info.get("stock_cost", 0), P, "stock_cost"),
+                initial_supply=info.get("initial_supply", None),
+                initial_shipments=info.get("initial_shipments", None),
+                dests=[], ship_capacity=[], dest_costs=[[] for _ in range(P)],
+            )
+            nd["n_supply"] = sum(1 for c in nd["supply_capacity"] if c > 0)
+            nodes.append(nd)
+        for name in names:                                                            # define_destinations
+            info = nodes_info[name]
+            if "destinations" not in info:
+                continue
+            nd = nodes[index[name]]
+            nd["dests"] = [index[d] for d in info["destinations"]]
+            nd["ship_capacity"] = list(info["ship_capacity"])
+            nd["dest_costs"] = [list(info["dest_costs"][p]) for p in range(P)]
+            for i, d in enumerate(nd["dests"]):
+                for p in range(P):
+                    nodes[d]["max_ship"][p] += nd["ship_capacity"][i]
+        a_off = lt_off = r_idx = 0
+        for nd in nodes:
+            nd["n_ship"] = sum(len(nd["dests"]) for p in range(P) if nd["stock_capacity"][p] > 0)
+            nd["action_offset"], nd["leadtime_offset"] = a_off, lt_off
+            a_off += nd["n_supply"] + nd["n_ship"]
+            lt_off += (P if nd["n_supply"] > 0 else 0) + len(nd["dests"])
+            nd["retailer_index"] = -1
+            if nd["last_level"]:
+                nd["retailer_index"] = r_idx
+                r_idx += 1
+        self.nodes = nodes
+        self.n_retailers = r_idx
+        self.n_actions = a_off
+        self.n_leadtimes = lt_off
+        self.n_obs = r_idx * P + len(nodes) * P + len(nodes) * P * self.avg_leadtime + 1      # :617-621
+
+    def node_table(self):
+        """The scg_sc_node array (host) for scg_sc_prepare and the device copy."""
+        P = self.P
+        table = (nat.ScNode * len(self.nodes))()
+        for i, nd in enumerate(self.nodes):
+            r = table[i]
+            r.last_level = int(nd["last_level"])
+            r.n_supply, r.n_ship, r.n_dests = nd["n_supply"], nd["n_ship"], len(nd["dests"])
+            if r.n_dests > _MAXD:
+                raise ValueError(f"node {nd['name']}: {r.n_dests} destinations (max {_MAXD})")
+            r.processing_capacity = _int("processing_capacity", nd["processing_capacity"])
+            r.retailer_index = nd["retailer_index"]
+            r.action_offset, r.leadtime_offset = nd["action_offset"], nd["leadtime_offset"]
+            for p in range(P):
+                r.supply_capacity[p] = _int("supply_capacity", nd["supply_capacity"][p])
+                r.supply_cost[p] = _int("supply_cost", nd["supply_cost"][p])
+                r.stock_capacity[p] = _int("stock_capacity", nd["stock_capacity"][p])
+                r.stock_cost[p] = _int("stock_cost", nd["stock_cost"][p])
+                r.processing_ratio[p] = _int("processing_ratio", nd["ratio"][p])
+                r.processing_cost[p] = _int("processing_cost", nd["processing_cost"][p])
+                r.max_ship[p] = _int("max_ship", nd["max_ship"][p])
+                r.initial_stock[p] = _int("initial_stock", nd["initial_stock"][p])
+                k = 0
+                for tbl in (nd["initial_supply"], nd["initial_shipments"]):                 # :405-412
+                    if tbl:
+                        for j, amount in enumerate(tbl[p]):
+                            if k >= _MAXI:
+                                raise ValueError(f"node {nd['name']}: more than {_MAXI} initial pipeline entries")
+                            r.init_time[p][k] = j + 1
+                            r.init_amount[p][k] = _int("initial pipeline amount", amount)
+                            k += 1
+                r.n_init[p] = k
+                for i_d in range(len(nd["dests"])):
+                    r.dest_costs[p][i_d] = _int("dest_costs", nd["dest_costs"][p][i_d])
+            for i_d, d in enumerate(nd["dests"]):
+                r.dests[i_d] = d
+                r.ship_capacity[i_d] = _int("ship_capacity", nd["ship_capacity"][i_d])
+        return table
+
+
+def _default_seed(seed):
+    if seed is None:  # RandomState(None) draws fresh entropy (:564); so do we
+        return int.from_bytes(os.urandom(8), "little")
+    return int(seed) & 0xFFFFFFFFFFFFFFFF
+
+
+class SupplyChainVecEnv:
+    """N lock-step SupplyChainEnv instances on one GPU.
+
+    reset() -> obs [N, n_obs]
+    step(actions float32 [N, n_actions] in [-1, 1]) -> (obs, reward float64 [N], done bool [N], info)
+
+    Returned tensors are this env's output buffers (clone() to keep them). With
+    auto_reset the terminal step resets every env in the same kernel; info then holds
+    'terminal_observation' and 'episode_return'.
+    """
+
+    def __init__(self, n_envs, nodes_info=None, spec=None, seed=0, device=None, env_offset=0, auto_reset=True,
+                 obs_dtype=torch.float32, track_returns=True, **kwargs):
+        if spec is None:
+            if nodes_info is None:
+                raise ValueError("pass nodes_info (+ SupplyChainEnv keywords) or a SupplyChainSpec")
+            spec = SupplyChainSpec(nodes_info, **kwargs)
+        elif kwargs:
+            raise ValueError("keywords go into the SupplyChainSpec when a spec is given")
+        n_envs = int(n_envs)
+        if n_envs < 1:
+            raise ValueError("n_envs must be >= 1")
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        if self.device.type != "cuda":
+            raise ValueError("SupplyChainVecEnv runs on a GPU device (no CPU fallback)")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self._dev_index = self.device.index
+        if obs_dtype not in (torch.float32, torch.float64):
+            raise ValueError("obs_dtype must be torch.float32 or torch.float64")
+        self.spec = spec
+        self.n_envs = n_envs
+        self.auto_reset = bool(auto_reset)
+        self.obs_dtype = obs_dtype
+        P, NN = spec.P, len(spec.nodes)
+
+        host_nodes = spec.node_table()
+        c = nat.ScConfig()
+        c.n_nodes, c.n_products, c.n_retailers = NN, P, spec.n_retailers
+        c.total_time_steps = spec.total_time_steps
+        c.avg_leadtime, c.max_leadtime = spec.avg_leadtime, spec.max_leadtime
+        c.stochastic_leadtimes = int(spec.stochastic_leadtimes)
+        c.demand_lo, c.demand_hi = spec.demand_range
+        for k, v in spec.penalties.items():
+            setattr(c, k, v)
+        c.obs_f64 = int(obs_dtype == torch.float64)
+        nat.check(nat.lib.scg_sc_prepare(ctypes.byref(c), host_nodes))
+        if (c.n_actions, c.n_obs, c.n_leadtimes) != (spec.n_actions, spec.n_obs, spec.n_leadtimes):
+            raise RuntimeError("host/library disagree on the chain's action/observation sizes")
+        self._node_bytes = torch.frombuffer(bytearray(bytes(host_nodes)), dtype=torch.uint8).to(self.device)
+        c.nodes = self._node_bytes.data_ptr()
+        if spec.stochastic_leadtimes:
+            thr = nat.poisson_table(spec.avg_leadtime - 1)
+            self._lt_thr = torch.tensor(np.asarray(thr, dtype=np.uint32).view(np.int32), device=self.device)
+            c.leadtime_poisson = self._lt_thr.data_ptr()
+            c.leadtime_poisson_len = len(thr)
+        self._cfg = c
+        self.n_actions, self.n_obs, self.heap_capacity = c.n_actions, c.n_obs, c.heap_capacity
+        NP, H = NN * P, c.heap_capacity
+        dev = self.device
+        self._stock = torch.zeros((NP, n_envs), dtype=torch.float64, device=dev)
+        self._heap_tk = torch.zeros((NP, H, n_envs), dtype=torch.int32, device=dev)
+        self._heap_val = torch.zeros((NP, H, n_envs), dtype=torch.float64, device=dev)
+        self._heap_size = torch.zeros((NP, n_envs), dtype=torch.int32, device=dev)
+        self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None
+        self._final_ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None
+        self._obs = torch.zeros((n_envs, c.n_obs), dtype=obs_dtype, device=dev)
+        self._term_obs = torch.zeros((n_envs, c.n_obs), dtype=obs_dtype, device=dev)
+        self._rew = torch.zeros(n_envs, dtype=torch.float64, device=dev)
+        self._done_false = torch.zeros(n_envs, dtype=torch.bool, device=dev)
+        self._done_true = torch.ones(n_envs, dtype=torch.bool, device=dev)
+        s = nat.ScState()
+        s.n_envs, s.env_offset, s.seed = n_envs, int(env_offset), _default_seed(seed)
+        s.episode, s.time_step = 0, -1
+        s.stock, s.heap_tk, s.heap_val = self._stock.data_ptr(), self._heap_tk.data_ptr(), self._heap_val.data_ptr()
+        s.heap_size, s.error_flags = self._heap_size.data_ptr(), self._err.data_ptr()
+        s.episode_return = self._ret.data_ptr() if track_returns else None
+        s.final_return = self._final_ret.data_ptr() if track_returns else None
+        self._st = s
+        self._cfg_ref, self._st_ref = ctypes.byref(self._cfg), ctypes.byref(self._st)
+        self._done_flag = ctypes.c_int32(0)
+        self._done_ref = ctypes.byref(self._done_flag)
+        self._flags = nat.SCG_BG_AUTORESET if self.auto_reset else 0
+        self._act_shape = (n_envs, c.n_actions)
+        self.single_action_space = spaces.Box(-1.0, 1.0, (c.n_actions,), np.float32)          # :625
+        self.single_observation_space = spaces.Box(-1.0, 1.0, (c.n_obs,), np.float32)         # :626
+
+    def _stream(self):
+        return nat.raw_stream(self._dev_index)
+
+    def seed(self, seed=None):
+        """New Philox key and episode counter 0 (the reference re-creates its RandomState, :811-813)."""
+        self._st.seed = _default_seed(seed)
+        self._st.episode = 0
+        self._st.time_step = -1
+
+    def reset(self):
+        nat.check(nat.lib.scg_sc_reset(self._cfg_ref, self._st_ref, self._obs.data_ptr(), self._stream()))
+        return self._obs
+
+    def _actions(self, a):
+        if not isinstance(a, torch.Tensor):
+            a = torch.as_tensor(np.asarray(a, dtype=np.float32))
+        if a.dtype != torch.float32 or a.device != self.device:
+            a = a.to(device=self.device, dtype=torch.float32)
+        if a.shape != self._act_shape:
+            if a.numel() != self._act_shape[0] * self._act_shape[1]:
+                raise ValueError(f"actions must have shape {self._act_shape}, got {tuple(a.shape)}")
+            a = a.reshape(self._act_shape)
+        return a.contiguous()
+
+    def step(self, actions):
+        a = actions
+        if not (type(a) is torch.Tensor and a.dtype is torch.float32 and a.is_cuda and
+                a.get_device() == self._dev_index and a.shape == self._act_shape and a.is_contiguous()):
+            a = self._actions(a)
+        rc = nat.lib.scg_sc_step(self._cfg_ref, self._st_ref, a.data_ptr(), self._obs.data_ptr(),
+                                 self._rew.data_ptr(), self._term_obs.data_ptr(), self._flags, self._done_ref,
+                                 self._stream())
+        if rc:
+            nat.check(rc)
+        if self._done_flag.value:
+            self.check_errors()
+            info = {"terminal_observation": self._term_obs}
+            if self._final_ret is not None:
+                info["episode_return"] = self._final_ret
+            return self._obs, self._rew, self._done_true, info
+        return self._obs, self._rew, self._done_false, {}
+
+    def check_errors(self):
+        """Raise if any env's in-transit heap overflowed its capacity (never expected: the
+        capacity is the chain's provable bound, scg_sc_prepare)."""
+        if int(self._err.item()):
+            raise RuntimeError("in-transit heap capacity exceeded; results are invalid")
+
+    def draw_tables(self, episode=None):
+        """(demand int32 [N, T+1, R, P], lead times int32 [N, T, n_lt] or None) for an episode."""
+        sp = self.spec
+        ep = self._st.episode if episode is None else int(episode)
+        dem = torch.empty((self.n_envs, sp.total_time_steps + 1, sp.n_retailers, sp.P), dtype=torch.int32,
+                          device=self.device)
+        lts = None
+        if sp.stochastic_leadtimes:
+            lts = torch.empty((self.n_envs, sp.total_time_steps, sp.n_leadtimes), dtype=torch.int32,
+                              device=self.device)
+        nat.check(nat.lib.scg_sc_draw_tables(self._cfg_ref, self._st_ref, ep, dem.data_ptr(),
+                                             lts.data_ptr() if lts is not None else None, self._stream()))
+        return dem, lts
+
+    # state views ----------------------------------------------------------------------
+    @property
+    def time_step(self):
+        return self._st.time_step
+
+    @property
+    def episode(self):
+        return self._st.episode
+
+    @property
+    def env_offset(self):
+        return self._st.env_offset
+
+    @property
+    def stock(self):
+        """[N, nodes, P] float64 view of every node's stock."""
+        return self._stock.view(len(self.spec.nodes), self.spec.P, self.n_envs).permute(2, 0, 1)
+
+    @property
+    def episode_return(self):
+        return self._ret
+
+    @property
+    def final_return(self):
+        return self._final_ret
+
+    def heaps(self, env):
+        """In-transit heaps of one env as the reference's shipments_by_prod lists
+        [node][product] -> [(time, amount), ...] in storage order."""
+        P = self.spec.P
+        tk = self._heap_tk[:, :, env].cpu().numpy()
+        val = self._heap_val[:, :, env].cpu().numpy()
+        size = self._heap_size[:, env].cpu().numpy()
+        out = []
+        for i in range(len(self.spec.nodes)):
+            out.append([[(int(tk[i * P + p, j]) >> 3, float(val[i * P + p, j])) for j in range(size[i * P + p])]
+                        for p in range(P)])
+        return out
+
+    def close(self):
+        pass
+
+
+class SupplyChainEnv:
+    """Drop-in for gym_supplychain.envs.SupplyChainEnv (:478-813), one env on the GPU.
+
+    Same constructor keywords; reset() -> float64 obs in [-1, 1]; step(action) ->
+    (obs, np.float64 reward, done, {}); seed(seed). Demand and stochastic lead times are
+    drawn with Philox from `seed` (see module docstring).
+    """
+
+    def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
+                 exceeded_process_capacity_cost=1000, exceeded_ship_capacity_cost=1000,
+                 demand_config_by_product=False, demand_range=(10, 20), demand_std=None, demand_sen_peaks=None,
+                 avg_demand_range=None, processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2,
+                 max_leadtime=2, total_time_steps=360, seed=None, build_info=False, demand_perturb_norm=False,
+                 device=None):
+        spec = SupplyChainSpec(nodes_info, num_products=num_products, unmet_demand_cost=unmet_demand_cost,
+                               exceeded_stock_capacity_cost=exceeded_stock_capacity_cost,
+                               exceeded_process_capacity_cost=exceeded_process_capacity_cost,
+                               exceeded_ship_capacity_cost=exceeded_ship_capacity_cost,
+                               demand_config_by_product=demand_config_by_product, demand_range=demand_range,
+                               demand_std=demand_std, demand_sen_peaks=demand_sen_peaks,
+                               avg_demand_range=avg_demand_range, processing_ratio=processing_ratio,
+                               stochastic_leadtimes=stochastic_leadtimes, avg_leadtime=avg_leadtime,
+                               max_leadtime=max_leadtime, total_time_steps=total_time_steps, seed=seed,
+                               build_info=build_info, demand_perturb_norm=demand_perturb_norm)
+        self._vec = SupplyChainVecEnv(1, spec=spec, seed=seed, device=device, auto_reset=False,
+                                      obs_dtype=torch.float64)
+        self.num_products = spec.P
+        self.total_time_steps = spec.total_time_steps
+        self.stochastic_leadtimes = spec.stochastic_leadtimes
+        self.avg_leadtime, self.max_leadtime = spec.avg_leadtime, spec.max_leadtime
+        self.demand_range = spec.demand_range
+        self.action_space = spaces.Box(-1.0, 1.0, (spec.n_actions,), np.float32)
+        self.observation_space = spaces.Box(-1.0, 1.0, (spec.n_obs,), np.float32)
+        self.current_state = None
+        self.current_reward = 0
+        pin = torch.cuda.is_available()
+        self._act_host = torch.zeros((1, spec.n_actions), dtype=torch.float32, pin_memory=pin)
+        self._act_np = self._act_host.numpy()
+        self._act_dev = torch.zeros((1, spec.n_actions), dtype=torch.float32, device=self._vec.device)
+        self._obs_host = torch.zeros((1, spec.n_obs), dtype=torch.float64, pin_memory=pin)
+        self._rew_host = torch.zeros(1, dtype=torch.float64, pin_memory=pin)
+
+    @property
+    def time_step(self):
+        return self._vec.time_step
+
+    def seed(self, seed=None):
+        self._vec.seed(seed)
+
+    def reset(self):
+        obs = self._vec.reset()
+        self.current_reward = 0
+        self.episode_rewards = 0
+        self.current_state = obs[0].cpu().numpy().copy()
+        return self.current_state
+
+    def step(self, action):
+        self._act_np[0, :] = np.asarray(action, dtype=np.float32).reshape(-1)
+        self._act_dev.copy_(self._act_host, non_blocking=True)
+        obs, rew, done, _ = self._vec.step(self._act_dev)
+        self._obs_host.copy_(obs, non_blocking=True)
+        self._rew_host.copy_(rew, non_blocking=True)
+        torch.cuda.current_stream(self._vec.device).synchronize()
+        self.current_state = self._obs_host.numpy()[0].copy()
+        self.current_reward = np.float64(self._rew_host.numpy()[0])
+        self.episode_rewards += self.current_reward
+        if self.time_step == self.total_time_steps:
+            self._vec.check_errors()
+        return self.current_state, self.current_reward, self.time_step == self.total_time_steps, {}
+
+    @property
+    def stock(self):
+        return self._vec.stock[0].cpu().numpy()
+
+    def shipments(self):
+        return self._vec.heaps(0)
+
+    def render(self, mode='human'):
+        print('TIMESTEP:', self.time_step)
+        st = self.stock
+        for i, name in enumerate(self._vec.spec.node_names):
+            print(f'{name} {self.shipments()[i]} [{np.round(st[i], 1)}]')
+        print('Current state :', self.current_state)
+        print('Current reward:', round(float(self.current_reward), 3))
+
+    def close(self):
+        pass

@@ -189,6 +189,108 @@ SCG_API int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, 
                      int32_t width, uint32_t tag, int32_t lo, int32_t hi, int32_t* out,
                      void* stream);
 
+/* ======================================================================================
+ * SupplyChainEnv (supplychain_env.py:478-813): generic multi-echelon, multi-product chain.
+ *
+ *   SupplyChainEnv.__init__(nodes_info, ...)  :482-628  -> scg_sc_config + scg_sc_node[] + scg_sc_prepare
+ *   SupplyChainEnv.reset()                    :630-682  -> scg_sc_reset
+ *   SupplyChainEnv.step(action)               :703-748  -> scg_sc_step
+ *     SC_Node.act :208-396, SC_Action.apply :42-98, heapq pipeline :398-400,
+ *     _build_observation :762-791, SC_Node.build_observation :428-463 (all fused)
+ * Per-episode randomness (customer demand table, stochastic lead times; the reference
+ * draws both with RandomState at reset, :644-672) is drawn on device with Philox:
+ * demand word (t*R + r)*P + p on stream 2, lead-time word (t-1)*n_lt + k on stream 3.
+ * ====================================================================================== */
+
+#define SCG_SC_MAX_PRODUCTS 8
+#define SCG_SC_MAX_DESTS 32
+#define SCG_SC_MAX_INIT 16
+#define SCG_SC_MAX_NODES 256
+#define SCG_STREAM_SC_DEMAND 2u
+#define SCG_STREAM_SC_LEADTIME 3u
+
+/* One chain node (SC_Node :106-206 after define_destinations), in nodes_info order. */
+typedef struct scg_sc_node {
+  int32_t last_level;           /* retailer: serves customer demand (:379-387)             */
+  int32_t n_supply;             /* SUPPLY actions: products with supply_capacity > 0       */
+  int32_t n_ship;               /* SHIP actions: n_dests per product with stock_capacity>0 */
+  int32_t n_dests;
+  int32_t processing_capacity;  /* > 0: a factory (:298-310, :337-341)                     */
+  int32_t retailer_index;       /* customer_demands column, -1 if not a retailer           */
+  int32_t action_offset;        /* first action of this node in the action vector (:716)  */
+  int32_t leadtime_offset;      /* first lead time of this node in a step's row (:720-722) */
+  int32_t supply_capacity[SCG_SC_MAX_PRODUCTS];
+  int32_t supply_cost[SCG_SC_MAX_PRODUCTS];
+  int32_t stock_capacity[SCG_SC_MAX_PRODUCTS];
+  int32_t stock_cost[SCG_SC_MAX_PRODUCTS];
+  int32_t processing_ratio[SCG_SC_MAX_PRODUCTS];
+  int32_t processing_cost[SCG_SC_MAX_PRODUCTS];
+  int32_t max_ship[SCG_SC_MAX_PRODUCTS];       /* observation normaliser (:147, :206)     */
+  int32_t initial_stock[SCG_SC_MAX_PRODUCTS];
+  int32_t n_init[SCG_SC_MAX_PRODUCTS];         /* initial pipeline entries (:402-412)     */
+  int32_t init_time[SCG_SC_MAX_PRODUCTS][SCG_SC_MAX_INIT];
+  int32_t init_amount[SCG_SC_MAX_PRODUCTS][SCG_SC_MAX_INIT];
+  int32_t dests[SCG_SC_MAX_DESTS];             /* node indices                            */
+  int32_t ship_capacity[SCG_SC_MAX_DESTS];
+  int32_t dest_costs[SCG_SC_MAX_PRODUCTS][SCG_SC_MAX_DESTS];
+} scg_sc_node;
+
+typedef struct scg_sc_config {
+  int32_t n_nodes, n_products, n_retailers;
+  int32_t n_actions;            /* action_space size (:608-610)                            */
+  int32_t n_obs;                /* observation_space size (:617-621)                       */
+  int32_t n_leadtimes;          /* lead times per step when stochastic (:601-605)          */
+  int32_t total_time_steps;     /* T                                                       */
+  int32_t avg_leadtime, max_leadtime, stochastic_leadtimes;
+  int32_t demand_lo, demand_hi; /* uniform demand range (demands_generator.py:33-36)       */
+  int32_t unmet_demand_cost, exceeded_stock_capacity_cost;
+  int32_t exceeded_process_capacity_cost, exceeded_ship_capacity_cost;
+  int32_t heap_capacity;        /* H: entries per (node, product) heap (scg_sc_prepare)    */
+  int32_t leadtime_poisson_len;
+  int32_t obs_f64;              /* observation dtype: 0 float32, 1 float64                 */
+  int32_t reserved;
+  const scg_sc_node* nodes;     /* DEVICE [n_nodes]                                        */
+  const uint32_t* leadtime_poisson; /* DEVICE Poisson(avg_leadtime-1) thresholds           */
+} scg_sc_config;
+
+/* Batch state. NP = n_nodes * n_products; per-env arrays are env-fastest. */
+typedef struct scg_sc_state {
+  int64_t n_envs;
+  int64_t env_offset;
+  uint64_t seed;
+  uint32_t episode;
+  int32_t time_step;            /* 0 after reset; -1 = not reset                           */
+  double* stock;                /* [NP][N]     float64 stock (:228)                        */
+  int32_t* heap_tk;             /* [NP][H][N]  time << 3 | NumPy kind of the amount        */
+  double* heap_val;             /* [NP][H][N]  amount                                       */
+  int32_t* heap_size;           /* [NP][N]                                                  */
+  double* episode_return;       /* [N] optional                                             */
+  double* final_return;         /* [N] optional: return at the terminal step                */
+  int32_t* error_flags;         /* [1] DEVICE, sticky: bit 0 = a heap exceeded capacity    */
+} scg_sc_state;
+
+/* sizeof(scg_sc_node), sizeof(scg_sc_config), sizeof(scg_sc_state), to check FFI bindings. */
+SCG_API int scg_sc_struct_sizes(size_t* node_size, size_t* config_size, size_t* state_size);
+
+/* Validate cfg against the host copy of the node table; fills n_actions, n_obs,
+ * n_leadtimes and heap_capacity. Host only. */
+SCG_API int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* host_nodes);
+
+/* reset() for all envs (:630-682). obs: DEVICE [N][n_obs] (float32 or float64) or NULL. */
+SCG_API int scg_sc_reset(const scg_sc_config* cfg, scg_sc_state* st, void* obs, void* stream);
+
+/* step(action) for all envs (:703-748).
+ *   action DEVICE float32 [N][n_actions], in the reference's [-1, 1] convention (:697-698)
+ *   obs    DEVICE [N][n_obs]; reward DEVICE float64 [N]; terminal_obs optional.
+ * Returns SCG_ERR_PAST_HORIZON after the terminal step without SCG_BG_AUTORESET. */
+SCG_API int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action, void* obs,
+                        double* reward, void* terminal_obs, uint32_t flags, int32_t* done, void* stream);
+
+/* The per-episode tables scg_sc_step draws (for tests): demand DEVICE int32
+ * [N][T+1][R][P], leadtimes DEVICE int32 [N][T][n_leadtimes] (NULL when deterministic). */
+SCG_API int scg_sc_draw_tables(const scg_sc_config* cfg, const scg_sc_state* st, uint32_t episode,
+                               int32_t* demand, int32_t* leadtimes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

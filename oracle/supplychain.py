@@ -1,0 +1,296 @@
+"""SupplyChainEnv CPU oracle — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Restatement of the generic multi-echelon supply chain of the reference
+(gym_supplychain/envs/supplychain_env.py, snapshot 2024-08-07): SC_Action.apply (:42-98),
+SC_Node.act (:208-396), heap pipeline (:398-400), SC_Node.build_observation (:428-463),
+SupplyChainEnv.step/_build_observation (:703-791).
+
+Numerics are part of the contract, so this restatement keeps the
+reference's operand types: float32 actions, Python-int capacities and costs, float64
+stock, np.int64 demands, and the in-transit pipeline as a CPython `heapq` list of
+(time, amount) tuples walked in storage order by the observation. NumPy 2 (NEP 50)
+promotion then yields the same float32/float64 intermediates as the reference, which
+the GPU kernel reproduces with tagged scalars (gym-supplychain_amd/csrc/scg_npscalar.h).
+
+Randomness is an input here: `reset(customer_demands, leadtimes)` takes the per-episode
+demand table [T+1, R, P] and lead-time table [T, n_lt] instead of drawing them from
+RandomState (:644-672); the GPU draws both with Philox (oracle/sc_draws.py).
+
+Pinned by tests/golden/sc_*.npz, written by oracle/gen_golden_sc.py from the reference.
+"""
+import heapq
+
+import numpy as np
+
+
+def _per_product(value, n_products, what):
+    """SC_Node._treat_int_or_list_param (:178-191): int -> replicated list."""
+    if type(value) is list:
+        if len(value) == 0:
+            return [0] * n_products
+        if len(value) != n_products:
+            raise AssertionError(f"{what}: expected {n_products} values")
+        return list(value)
+    if type(value) is int:
+        return [value] * n_products
+    raise ValueError(f"Invalid param: '{value}' should be an int or a list with one value per product")
+
+
+class _Node:
+    """Static description + dynamic state of one chain node (SC_Node, :106-206)."""
+
+    def __init__(self, name, info, n_products, processing_ratio, penalties, max_leadtime):
+        P = n_products
+        self.name = name
+        self.P = P
+        proc_cost = info.get("processing_cost", 0)
+        no_processing = ((type(proc_cost) is int and proc_cost == 0) or
+                         (type(proc_cost) is list and sum(proc_cost) == 0))       # :518-522
+        self.ratio = _per_product(0 if no_processing else processing_ratio, P, "processing_ratio")
+        self.processing_cost = _per_product(proc_cost, P, "processing_cost")
+        self.processing_capacity = info.get("processing_capacity", 0)
+        supply_cap = _per_product(info.get("supply_capacity", 0), P, "supply_capacity")
+        self.supply_cost = _per_product(info.get("supply_cost", 0), P, "supply_cost")
+        # a SUPPLY action per product with positive capacity (:137-147)
+        self.supply_cap = supply_cap if max(supply_cap) > 0 else [0] * P
+        self.n_supply = sum(1 for c in self.supply_cap if c > 0)
+        self.max_ship = list(supply_cap) if max(supply_cap) > 0 else [0] * P
+        self.initial_stock = _per_product(info.get("initial_stock", 0), P, "initial_stock")
+        self.initial_supply = info.get("initial_supply", None)
+        self.initial_shipments = info.get("initial_shipments", None)
+        self.stock_cap = _per_product(info.get("stock_capacity", float("inf")), P, "stock_capacity")
+        self.stock_cost = _per_product(info.get("stock_cost", 0), P, "stock_cost")
+        self.last_level = info.get("last_level", False)
+        self.pen_stock, self.pen_process, self.pen_ship, self.pen_unmet = penalties
+        self.max_leadtime = max_leadtime
+        self.dests = []
+        self.ship_cap = []
+        self.dest_costs = None
+        self.n_ship = 0
+        self.has_ship = [False] * P
+
+    def connect(self, dests, ship_capacity, dest_costs):
+        """define_destinations (:193-206)."""
+        self.dests = dests
+        self.ship_cap = ship_capacity
+        self.dest_costs = dest_costs
+        for p, cap in enumerate(self.stock_cap):
+            self.has_ship[p] = cap > 0
+            if cap > 0:
+                self.n_ship += len(dests)
+        for i, d in enumerate(dests):
+            for p in range(d.P):
+                d.max_ship[p] += ship_capacity[i]
+
+    @property
+    def n_actions(self):
+        return self.n_supply + self.n_ship
+
+    # --------------------------------------------------------------------------------
+    def reset(self):
+        """SC_Node.reset (:402-412): initial pipeline at times 1..k."""
+        self.stock = self.initial_stock
+        self.heaps = [[] for _ in range(self.P)]
+        for table in (self.initial_supply, self.initial_shipments):
+            if table:
+                for p in range(self.P):
+                    for i, amount in enumerate(table[p]):
+                        heapq.heappush(self.heaps[p], (i + 1, amount))
+
+
+def _split_shipment(values, limit, unit_costs):
+    """SC_Action.apply for SHIP (:58-96): cut [0, limit] at the sorted action values."""
+    amounts = [0] * len(values)
+    left = limit
+    if left > 0:
+        prev = 0
+        for v, i in sorted((values[i], i) for i in range(len(values))):
+            amt = (v - prev) * limit
+            if amt > left:
+                amt = left
+            amounts[i] = amt
+            left -= amt
+            prev = v
+    return amounts
+
+
+def _node_act(nd, actions, leadtimes, t, demand):
+    """SC_Node.act (:208-396). Returns the node's cost; mutates nd.stock / heaps."""
+    P = nd.P
+    cost = 0
+    lt_i = 0
+    received = np.zeros(P)
+    for p, heap in enumerate(nd.heaps):                                   # :222-225
+        while heap and heap[0][0] == t:
+            received[p] += heapq.heappop(heap)[1]
+    nd.stock += received                                                  # :228
+    for p in range(P):                                                    # :232-240
+        if nd.stock[p] > nd.stock_cap[p]:
+            cost += nd.pen_stock * (nd.stock[p] - nd.stock_cap[p])
+            nd.stock[p] = nd.stock_cap[p]
+    a_i = 0
+    if nd.n_supply > 0:                                                   # :244-259
+        for p in range(P):
+            if nd.supply_cap[p] > 0:
+                amount = actions[a_i] * nd.supply_cap[p]
+                c = amount * nd.supply_cost[p]
+                a_i += 1
+                if amount > 0:
+                    heapq.heappush(nd.heaps[p], (t + leadtimes[lt_i], amount))
+                    lt_i += 1                       # cursor advances only on a shipment (:252-254)
+                cost += c
+    if not nd.last_level:                                                 # :262-375
+        ship_left = nd.ship_cap.copy()
+        proc_left = nd.processing_capacity
+        lt_base = lt_i
+        D = len(nd.dests)
+        for p in range(P):
+            if not nd.has_ship[p]:
+                continue
+            over_ship = 0
+            over_proc = 0
+            material = nd.stock[p]
+            if material > 0:
+                limit = min(nd.stock_cap[p], material)                   # :61-64
+                out = _split_shipment(actions[a_i:a_i + D], limit, nd.dest_costs[p])
+                sent = out.copy()
+                if nd.processing_capacity > 0:                            # :298-310
+                    for i, amt in enumerate(out):
+                        if amt > 0:
+                            if amt > proc_left:
+                                over_proc += amt - proc_left
+                                out[i] = proc_left
+                            proc_left -= out[i]
+                        sent[i] = out[i] / nd.ratio[p]
+                for i, amt in enumerate(sent):                            # :312-328
+                    if amt > 0 and amt > ship_left[i]:
+                        over_ship += amt - ship_left[i]
+                        sent[i] = ship_left[i]
+                        out[i] = sent[i] * nd.ratio[p] if nd.processing_capacity > 0 else sent[i]
+                        ship_left[i] -= out[i]            # decremented only on overflow, by out[i]
+                leaving = sum(out)                                        # :331-332
+                nd.stock[p] -= leaving
+                if nd.processing_capacity > 0:                            # :337-341
+                    cost += leaving * nd.processing_cost[p]
+                for i in range(D):                                        # :344-348
+                    if sent[i] > 0:
+                        heapq.heappush(nd.dests[i].heaps[p], (t + leadtimes[lt_i], sent[i]))
+                    lt_i += 1
+                cost += sum(sent[i] * nd.dest_costs[p][i] for i in range(D))   # :352-353
+            cost += nd.pen_process * over_proc                            # :361
+            cost += nd.pen_ship * over_ship                               # :366
+            a_i += D
+            lt_i = lt_base                       # same lead times for every product (:375)
+    else:                                                                 # :379-387
+        for p in range(P):
+            served = min(nd.stock[p], demand[p])
+            nd.stock[p] -= served
+            cost += nd.pen_unmet * (demand[p] - served)
+    for p in range(P):                                                    # :390-394
+        cost += nd.stock[p] * nd.stock_cost[p]
+    return cost
+
+
+def _node_obs(nd, first, last):
+    """SC_Node.build_observation (:428-463): stock share, then in-transit bins per
+    product for times first..last-1 and 'last or later', walking the heap list in its
+    storage order (which is not time-sorted: SURVEY F9)."""
+    vals = [nd.stock[i] / nd.stock_cap[i] for i in range(len(nd.stock))]
+    for p, heap in enumerate(nd.heaps):
+        if not heap:
+            vals += [0] * (last - first + 1)
+            continue
+        k = 0
+        for when in range(first, last):
+            vals.append(0)
+            while k < len(heap) and heap[k][0] == when:
+                vals[-1] += heap[k][1]
+                k += 1
+            vals[-1] /= nd.max_ship[p]
+        vals.append(0)
+        while k < len(heap):
+            vals[-1] += heap[k][1]
+            k += 1
+        vals[-1] /= nd.max_ship[p] * (nd.max_leadtime - (last - first))
+    return vals
+
+
+class SupplyChainOracle:
+    """SupplyChainEnv (:478-813) with demand / lead-time tables supplied per episode."""
+
+    def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
+                 exceeded_process_capacity_cost=1000, exceeded_ship_capacity_cost=1000, demand_range=(10, 20),
+                 processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2, max_leadtime=2,
+                 total_time_steps=360):
+        P = num_products
+        pens = (exceeded_stock_capacity_cost, exceeded_process_capacity_cost, exceeded_ship_capacity_cost,
+                unmet_demand_cost)
+        by_name = {}
+        self.nodes = []
+        for name, info in nodes_info.items():
+            nd = _Node(name, info, P, processing_ratio, pens, max_leadtime)
+            by_name[name] = nd
+            self.nodes.append(nd)
+        for name, info in nodes_info.items():
+            if "destinations" in info:
+                by_name[name].connect([by_name[d] for d in info["destinations"]], info["ship_capacity"],
+                                      info["dest_costs"])
+        self.retailers = [nd for nd in self.nodes if nd.last_level]
+        self.P = P
+        self.T = total_time_steps
+        self.lo, self.hi = demand_range
+        if self.lo == self.hi:
+            raise AssertionError("demand_range must not be empty")             # :592
+        self.stochastic = stochastic_leadtimes
+        self.avg_lt = avg_leadtime
+        self.max_lt = max_leadtime
+        self.n_lt = sum((P if nd.n_supply > 0 else 0) + len(nd.dests) for nd in self.nodes)   # :601-605
+        self.action_size = sum(nd.n_actions for nd in self.nodes)
+        self.obs_size = len(self.retailers) * P + len(self.nodes) * P + len(self.nodes) * P * avg_leadtime + 1
+        self.low = np.full(self.obs_size, -1.0, dtype=np.float32)
+        self.high = np.full(self.obs_size, 1.0, dtype=np.float32)
+
+    def reset(self, customer_demands, leadtimes=None):
+        for nd in self.nodes:
+            nd.reset()
+        self.t = 0
+        self.demands = np.asarray(customer_demands, dtype=np.int64).reshape(self.T + 1, len(self.retailers), self.P)
+        if self.stochastic:
+            self.leadtimes = np.asarray(leadtimes, dtype=np.int64).reshape(self.T, self.n_lt)
+        self.episode_rewards = 0
+        return self._obs()
+
+    def step(self, action):
+        a = (action + 1) / 2                                                  # :697-698
+        self.t += 1
+        total = 0
+        a_i = lt_i = r_i = 0
+        for nd in self.nodes:                                                 # :714-736
+            acts = a[a_i:a_i + nd.n_actions]
+            a_i += nd.n_actions
+            if self.stochastic:
+                k = nd.n_supply + nd.n_ship // self.P
+                lts = self.leadtimes[self.t - 1, lt_i:lt_i + k]
+                lt_i += k
+            else:
+                lts = nd.n_actions * [self.avg_lt]
+            demand = None
+            if nd.last_level:
+                demand = self.demands[self.t - 1, r_i]
+                r_i += 1
+            total += _node_act(nd, acts, lts, self.t, demand)
+        reward = -total
+        self.episode_rewards += reward
+        return self._obs(), reward, self.t == self.T, {}
+
+    def _obs(self):                                                           # :762-791
+        dem = (self.demands[self.t, :].flatten() - self.lo) / (self.hi - self.lo)
+        nodes = []
+        for nd in self.nodes:
+            nodes += _node_obs(nd, self.t + 1, self.t + self.avg_lt)
+        x = np.concatenate((dem, nodes, [(self.T - self.t) / self.T]))
+        return np.clip(x * 2 - 1, self.low, self.high)
+
+    def heaps(self):
+        """[node][product] -> list of (time, amount) in storage order (for parity tests)."""
+        return [[list(h) for h in nd.heaps] for nd in self.nodes]

@@ -22,3 +22,21 @@ def load_beergame(name):
     g["info"] = info
     g["is_poisson"] = float(g["lam"]) >= 0
     return g
+
+
+# ---- SupplyChain (written by oracle/gen_golden_sc.py) ----------------------------------
+SC_ORACLE_KW = ("num_products", "unmet_demand_cost", "exceeded_stock_capacity_cost", "exceeded_process_capacity_cost",
+                "exceeded_ship_capacity_cost", "demand_range", "processing_ratio", "stochastic_leadtimes",
+                "avg_leadtime", "max_leadtime", "total_time_steps")
+
+
+def sc_cases():
+    return sorted(os.path.basename(p)[len("sc_"):-4] for p in glob.glob(os.path.join(GOLDEN, "sc_*.npz")))
+
+
+def load_sc(name):
+    import json
+    g = dict(np.load(os.path.join(GOLDEN, f"sc_{name}.npz")))
+    g["meta"] = json.loads(str(g["meta"]))
+    g["oracle_kwargs"] = {k: g["meta"]["kwargs"][k] for k in SC_ORACLE_KW if k in g["meta"]["kwargs"]}
+    return g

@@ -1,0 +1,66 @@
+// TEST-ONLY host build of the SupplyChain kernel body (gym-supplychain_amd/csrc/
+// scg_supplychain_core.h, __host__ __device__) so the CPU suite can check the exact code
+// the GPU runs against the reference's golden vectors without a GPU. Never part of the
+// product: libscgpu.so has no CPU path, and this library is built by the tests only.
+#include <cstring>
+
+#include "scg_supplychain_core.h"
+
+extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                           uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
+                           double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
+                           int32_t* heap_size) {
+  scg::ScCtx c;
+  std::memset(&c, 0, sizeof(c));
+  c.nodes = nodes;
+  c.lt_thr = lt_thr;
+  c.n_nodes = cfg->n_nodes;
+  c.P = cfg->n_products;
+  c.R = cfg->n_retailers;
+  c.A = cfg->n_actions;
+  c.O = cfg->n_obs;
+  c.H = cfg->heap_capacity;
+  c.T = cfg->total_time_steps;
+  c.avg_lt = cfg->avg_leadtime;
+  c.max_lt = cfg->max_leadtime;
+  c.stochastic = cfg->stochastic_leadtimes;
+  c.n_lt = cfg->n_leadtimes;
+  c.lt_thr_len = cfg->leadtime_poisson_len;
+  c.lo = cfg->demand_lo;
+  c.hi = cfg->demand_hi;
+  c.pen_unmet = cfg->unmet_demand_cost;
+  c.pen_stock = cfg->exceeded_stock_capacity_cost;
+  c.pen_proc = cfg->exceeded_process_capacity_cost;
+  c.pen_ship = cfg->exceeded_ship_capacity_cost;
+  c.key0 = static_cast<uint32_t>(seed & 0xffffffffu);
+  c.key1 = static_cast<uint32_t>(seed >> 32);
+  const int NP = c.n_nodes * c.P;
+  // one env, stride 1: the state lives in the last snapshot slot and is copied out per step
+  double* st = stock;
+  int32_t* tk = heap_tk;
+  double* val = heap_val;
+  int32_t* sz = heap_size;
+  scg::ScEnv e{st, tk, val, sz, 1, env_id, episode, 0};
+  scg::sc_reset_env(c, e);
+  auto sink = [&](double* row) { return [row](int o, double x) { row[o] = x; }; };
+  {
+    auto out = sink(obs);
+    scg::sc_observe(c, e, 0, out);
+  }
+  for (int t = 1; t <= steps; ++t) {
+    // copy state snapshot t-1 -> t, then advance snapshot t in place
+    std::memcpy(stock + t * NP, stock + (t - 1) * NP, sizeof(double) * NP);
+    std::memcpy(heap_tk + static_cast<int64_t>(t) * NP * c.H, heap_tk + static_cast<int64_t>(t - 1) * NP * c.H,
+                sizeof(int32_t) * NP * c.H);
+    std::memcpy(heap_val + static_cast<int64_t>(t) * NP * c.H, heap_val + static_cast<int64_t>(t - 1) * NP * c.H,
+                sizeof(double) * NP * c.H);
+    std::memcpy(heap_size + t * NP, heap_size + (t - 1) * NP, sizeof(int32_t) * NP);
+    scg::ScEnv et{stock + t * NP, heap_tk + static_cast<int64_t>(t) * NP * c.H,
+                  heap_val + static_cast<int64_t>(t) * NP * c.H, heap_size + t * NP, 1, env_id, episode, 0};
+    rewards[t - 1] = scg::sc_step_env(c, et, actions + static_cast<int64_t>(t - 1) * c.A, t);
+    auto out = sink(obs + static_cast<int64_t>(t) * c.O);
+    scg::sc_observe(c, et, t, out);
+    if (et.overflow) return 1;
+  }
+  return e.overflow;
+}

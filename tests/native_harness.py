@@ -1,0 +1,47 @@
+"""Builds tests/native/sc_host_harness.cpp (test-only host build of the SupplyChain kernel
+body) with hipcc and binds it with ctypes. Used by tests/test_sc_host.py."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from conftest import PKG_ROOT, REPO
+
+SRC = os.path.join(REPO, "tests", "native", "sc_host_harness.cpp")
+OUT = os.path.join(REPO, "tests", "native", "_build", "libsc_host.so")
+CSRC = os.path.join(PKG_ROOT, "csrc")
+
+
+def build():
+    deps = [SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
+        [os.path.join(REPO, "include", "scgpu.h")]
+    if not (os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps)):
+        os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        subprocess.run(["hipcc", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off",
+                        "--offload-arch=gfx950", "-I", os.path.join(REPO, "include"), "-I", CSRC,
+                        "-o", OUT, SRC], check=True)
+    lib = ctypes.CDLL(OUT)
+    lib.sch_episode.restype = ctypes.c_int
+    return lib
+
+
+def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions):
+    """Reset + len(actions) steps of one env; returns obs [T+1, O], rewards [T],
+    stock [T+1, NP], heaps (tk, val, size) per snapshot."""
+    T = actions.shape[0]
+    NP = cfg.n_nodes * cfg.n_products
+    H = cfg.heap_capacity
+    obs = np.zeros((T + 1, cfg.n_obs))
+    rew = np.zeros(T)
+    stock = np.zeros((T + 1, NP))
+    tk = np.zeros((T + 1, NP, H), dtype=np.int32)
+    val = np.zeros((T + 1, NP, H))
+    size = np.zeros((T + 1, NP), dtype=np.int32)
+    thr = np.asarray(lt_thr if lt_thr is not None else [0], dtype=np.uint32)
+    acts = np.ascontiguousarray(actions, dtype=np.float32)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rc = lib.sch_episode(ctypes.byref(cfg), nodes, p(thr), ctypes.c_uint64(seed), ctypes.c_uint32(env_id),
+                         ctypes.c_uint32(episode), ctypes.c_int32(T), p(acts), p(obs), p(rew), p(stock), p(tk),
+                         p(val), p(size))
+    return rc, obs, rew, stock, (tk, val, size)

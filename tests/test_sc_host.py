@@ -1,0 +1,66 @@
+"""The SupplyChain kernel body (scg_supplychain_core.h), compiled for the HOST by the
+test-only harness tests/native/sc_host_harness.cpp, against the reference's golden
+vectors: observations, rewards, stocks and heap storage order, bit for bit. This checks
+the exact arithmetic the GPU kernel runs (NumPy-2 promotion emulation, heapq
+restatement, Philox draws) on the CPU suite; the GPU parity tests repeat it on device.
+"""
+import numpy as np
+import pytest
+
+from golden_io import load_sc, sc_cases
+
+CASES = sc_cases()
+
+
+@pytest.fixture(scope="module")
+def harness():
+    import native_harness
+    return native_harness.build()
+
+
+def _setup(g):
+    import ctypes
+    from gym_supplychain_amd import _native as nat
+    from gym_supplychain_amd.envs import SupplyChainSpec
+    meta = g["meta"]
+    spec = SupplyChainSpec(meta["nodes_info"], **meta["kwargs"])
+    nodes = spec.node_table()
+    c = nat.ScConfig()
+    c.n_nodes, c.n_products, c.n_retailers = len(spec.nodes), spec.P, spec.n_retailers
+    c.total_time_steps, c.avg_leadtime, c.max_leadtime = spec.total_time_steps, spec.avg_leadtime, spec.max_leadtime
+    c.stochastic_leadtimes = int(spec.stochastic_leadtimes)
+    c.demand_lo, c.demand_hi = spec.demand_range
+    for k, v in spec.penalties.items():
+        setattr(c, k, v)
+    thr = None
+    if spec.stochastic_leadtimes:
+        thr = nat.poisson_table(spec.avg_leadtime - 1)
+        c.leadtime_poisson_len = len(thr)
+    assert nat.lib.scg_sc_prepare(ctypes.byref(c), nodes) == 0, nat.last_error()
+    return spec, c, nodes, thr
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_host_build_of_kernel_body_matches_reference(harness, name):
+    import native_harness
+    g = load_sc(name)
+    meta = g["meta"]
+    spec, c, nodes, thr = _setup(g)
+    N = g["obs"].shape[1]
+    P, H = spec.P, c.heap_capacity
+    for n in range(N):
+        rc, obs, rew, stock, (tk, val, size) = native_harness.run_episode(harness, c, nodes, thr, meta["seed"], n, 0,
+                                                                           g["actions"][:, n])
+        assert rc == 0
+        assert np.array_equal(obs, g["obs"][:, n]), name
+        assert np.array_equal(rew, g["reward"][:, n]), name
+        assert np.array_equal(stock.reshape(stock.shape[0], -1, P), g["stock"][:, n])
+        gt = g["heap_t"][:, n].reshape(len(obs), -1, g["heap_t"].shape[-1])
+        gv = g["heap_v"][:, n].reshape(gt.shape)
+        for s in range(len(obs)):
+            for hp in range(gt.shape[1]):
+                k = int(size[s, hp])
+                assert k == int((gt[s, hp] >= 0).sum())
+                assert (tk[s, hp, :k] >> 3).tolist() == gt[s, hp, :k].tolist()
+                assert val[s, hp, :k].tolist() == gv[s, hp, :k].tolist()
+        assert H >= gt.shape[-1]
