@@ -55,7 +55,7 @@ struct ObsRow {
 };
 
 __device__ __forceinline__ ScEnv env_view(const ScArgs& a, int64_t n, uint32_t episode) {
-  return ScEnv{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, static_cast<uint32_t>(a.env_offset + n), episode, 0};
+  return ScEnv{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
 }
 
 __global__ __launch_bounds__(kScBlock) void sc_reset_kernel(const ScArgs a) {
@@ -128,7 +128,7 @@ int sc_check(const scg_sc_config* cfg, const scg_sc_state* st) {
   if (!cfg || !st) return fail(SCG_ERR_INVALID, "null config/state");
   if (!cfg->nodes || cfg->heap_capacity <= 0 || cfg->n_obs <= 0)
     return fail(SCG_ERR_INVALID, "config not prepared (call scg_sc_prepare) or no device node table");
-  if (cfg->stochastic_leadtimes && !cfg->leadtime_poisson)
+  if (cfg->stochastic_leadtimes && !cfg->leadtime_poisson && !cfg->leadtime_table)
     return fail(SCG_ERR_INVALID, "stochastic lead times need the Poisson threshold table");
   if (st->n_envs <= 0) return fail(SCG_ERR_INVALID, "n_envs must be > 0");
   if (st->env_offset < 0 || st->env_offset + st->n_envs > (int64_t(1) << 32))
@@ -144,6 +144,8 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   ScCtx& c = a.c;
   c.nodes = cfg->nodes;
   c.lt_thr = cfg->leadtime_poisson;
+  c.dem_tab = cfg->demand_table;
+  c.lt_tab = cfg->leadtime_table;
   c.n_nodes = cfg->n_nodes;
   c.P = cfg->n_products;
   c.R = cfg->n_retailers;

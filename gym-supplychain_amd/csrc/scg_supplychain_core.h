@@ -22,6 +22,8 @@ namespace scg {
 struct ScCtx {
   const scg_sc_node* nodes;
   const uint32_t* lt_thr;
+  const int32_t* dem_tab;  // [N][T+1][R][P] or null (Philox)
+  const int32_t* lt_tab;   // [N][T][n_lt] or null (Philox)
   int32_t n_nodes, P, R, A, O, H, T;
   int32_t avg_lt, max_lt, stochastic, n_lt, lt_thr_len;
   int32_t lo, hi;
@@ -37,6 +39,7 @@ struct ScEnv {
   int32_t* size;     // [NP]
   int64_t stride;    // envs in the batch
   uint32_t env_id;   // global id (Philox counter)
+  int64_t local;     // index in this shard (caller tables)
   uint32_t episode;
   int32_t overflow;  // set when a push met a full heap (the push is dropped)
 };
@@ -77,6 +80,7 @@ __host__ __device__ __forceinline__ uint32_t cached_word(const ScCtx& c, const S
 __host__ __device__ __forceinline__ int32_t sc_demand(const ScCtx& c, const ScEnv& e, WordCache& wc, int row, int r,
                                                       int p) {
   const uint32_t j = static_cast<uint32_t>((row * c.R + r) * c.P + p);
+  if (c.dem_tab) return c.dem_tab[e.local * (static_cast<int64_t>(c.T + 1) * c.R * c.P) + j];
   const uint32_t u = cached_word(c, e, wc, j, SCG_STREAM_SC_DEMAND);
   const uint64_t span = static_cast<uint64_t>(c.hi - c.lo + 1);
   return c.lo + static_cast<int32_t>((static_cast<uint64_t>(u) * span) >> 32);
@@ -85,6 +89,7 @@ __host__ __device__ __forceinline__ int32_t sc_demand(const ScCtx& c, const ScEn
 // leadtimes[t-1, k]: clip(1 + Poisson(avg-1), 1, max)   (:670-672)
 __host__ __device__ __forceinline__ int32_t sc_leadtime(const ScCtx& c, const ScEnv& e, WordCache& wc, int t, int k) {
   const uint32_t j = static_cast<uint32_t>((t - 1) * c.n_lt + k);
+  if (c.lt_tab) return c.lt_tab[e.local * (static_cast<int64_t>(c.T) * c.n_lt) + j];
   const uint32_t u = cached_word(c, e, wc, j, SCG_STREAM_SC_LEADTIME);
   int32_t x = 0;
   for (int i = 0; i < c.lt_thr_len; ++i) x += (c.lt_thr[i] <= u) ? 1 : 0;

@@ -118,7 +118,8 @@ class ScConfig(ctypes.Structure):
         "avg_leadtime", "max_leadtime", "stochastic_leadtimes", "demand_lo", "demand_hi", "unmet_demand_cost",
         "exceeded_stock_capacity_cost", "exceeded_process_capacity_cost", "exceeded_ship_capacity_cost",
         "heap_capacity", "leadtime_poisson_len", "obs_f64", "reserved")] + [
-        ("nodes", ctypes.c_void_p), ("leadtime_poisson", ctypes.c_void_p)]
+        ("nodes", ctypes.c_void_p), ("leadtime_poisson", ctypes.c_void_p), ("demand_table", ctypes.c_void_p),
+        ("leadtime_table", ctypes.c_void_p)]
 
 
 class ScState(ctypes.Structure):

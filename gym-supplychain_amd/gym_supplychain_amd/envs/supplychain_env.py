@@ -203,10 +203,14 @@ class SupplyChainVecEnv:
     Returned tensors are this env's output buffers (clone() to keep them). With
     auto_reset the terminal step resets every env in the same kernel; info then holds
     'terminal_observation' and 'episode_return'.
+
+    demand_table / leadtime_table: optional device int32 tensors [N, T+1, R, P] /
+    [N, T, n_lt] used for every episode instead of the Philox draws (e.g. to replay the
+    reference's RandomState episodes exactly).
     """
 
     def __init__(self, n_envs, nodes_info=None, spec=None, seed=0, device=None, env_offset=0, auto_reset=True,
-                 obs_dtype=torch.float32, track_returns=True, **kwargs):
+                 obs_dtype=torch.float32, track_returns=True, demand_table=None, leadtime_table=None, **kwargs):
         if spec is None:
             if nodes_info is None:
                 raise ValueError("pass nodes_info (+ SupplyChainEnv keywords) or a SupplyChainSpec")
@@ -250,6 +254,21 @@ class SupplyChainVecEnv:
             self._lt_thr = torch.tensor(np.asarray(thr, dtype=np.uint32).view(np.int32), device=self.device)
             c.leadtime_poisson = self._lt_thr.data_ptr()
             c.leadtime_poisson_len = len(thr)
+        T, R = spec.total_time_steps, spec.n_retailers
+        if demand_table is not None:
+            if (demand_table.device != self.device or demand_table.dtype != torch.int32 or
+                    tuple(demand_table.shape) != (n_envs, T + 1, R, P)):
+                raise ValueError(f"demand_table must be int32 [{n_envs}, {T + 1}, {R}, {P}] on {self.device}")
+            self._dem_tab = demand_table.contiguous()
+            c.demand_table = self._dem_tab.data_ptr()
+        if leadtime_table is not None:
+            if not spec.stochastic_leadtimes:
+                raise ValueError("leadtime_table needs stochastic_leadtimes=True")
+            if (leadtime_table.device != self.device or leadtime_table.dtype != torch.int32 or
+                    tuple(leadtime_table.shape) != (n_envs, T, spec.n_leadtimes)):
+                raise ValueError(f"leadtime_table must be int32 [{n_envs}, {T}, {spec.n_leadtimes}] on {self.device}")
+            self._lt_tab = leadtime_table.contiguous()
+            c.leadtime_table = self._lt_tab.data_ptr()
         self._cfg = c
         self.n_actions, self.n_obs, self.heap_capacity = c.n_actions, c.n_obs, c.heap_capacity
         NP, H = NN * P, c.heap_capacity

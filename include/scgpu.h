@@ -251,6 +251,9 @@ typedef struct scg_sc_config {
   int32_t reserved;
   const scg_sc_node* nodes;     /* DEVICE [n_nodes]                                        */
   const uint32_t* leadtime_poisson; /* DEVICE Poisson(avg_leadtime-1) thresholds           */
+  const int32_t* demand_table;  /* DEVICE [N][T+1][R][P] caller tables instead of Philox    */
+                                /* (NULL = draw; e.g. to replay RandomState episodes)       */
+  const int32_t* leadtime_table;/* DEVICE [N][T][n_leadtimes] likewise (stochastic only)    */
 } scg_sc_config;
 
 /* Batch state. NP = n_nodes * n_products; per-env arrays are env-fastest. */
