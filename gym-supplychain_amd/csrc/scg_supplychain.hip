@@ -71,11 +71,12 @@ __global__ __launch_bounds__(kScBlock) void sc_reset_kernel(const ScArgs a) {
   if (e.overflow) atomicOr(a.err, 1);
 }
 
+template <int MAXD>
 __global__ __launch_bounds__(kScBlock) void sc_step_kernel(const ScArgs a) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
   if (n >= a.n) return;
   ScEnv e = env_view(a, n, a.episode);
-  const double reward = sc_step_env(a.c, e, a.act + n * a.c.A, a.t);
+  const double reward = sc_step_env<MAXD>(a.c, e, a.act + n * a.c.A, a.t);
   a.rew[n] = reward;
   const bool terminal = a.flags & 1;
   if (a.ep_ret) {
@@ -245,13 +246,15 @@ int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
     }
   }
   const int lmax = cfg->stochastic_leadtimes ? cfg->max_leadtime : cfg->avg_leadtime;
-  int H = 1;
+  int H = 1, maxd = 0;
+  for (int i = 0; i < NN; ++i) maxd = std::max(maxd, nodes[i].n_dests);
   for (int i = 0; i < NN; ++i)
     for (int p = 0; p < P; ++p) H = std::max(H, indeg[i * P + p] * (lmax + 1) + nodes[i].n_init[p]);
   cfg->n_actions = n_act;
   cfg->n_leadtimes = n_lt;
   cfg->n_obs = n_ret * P + NN * P + NN * P * cfg->avg_leadtime + 1;
   cfg->heap_capacity = H;
+  cfg->max_dests = maxd;
   return SCG_OK;
 }
 
@@ -283,7 +286,15 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
   a.rew = reward;
   a.t = t;
   a.flags = (terminal ? 1 : 0) | (autoreset ? 2 : 0);
-  hipLaunchKernelGGL(sc_step_kernel, sc_grid(st->n_envs), dim3(kScBlock), 0, static_cast<hipStream_t>(stream), a);
+  const dim3 grid = sc_grid(st->n_envs);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (sc_maxd_bucket(cfg->max_dests)) {
+    case 2: hipLaunchKernelGGL(sc_step_kernel<2>, grid, dim3(kScBlock), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(sc_step_kernel<4>, grid, dim3(kScBlock), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(sc_step_kernel<8>, grid, dim3(kScBlock), 0, s, a); break;
+    case 16: hipLaunchKernelGGL(sc_step_kernel<16>, grid, dim3(kScBlock), 0, s, a); break;
+    default: hipLaunchKernelGGL(sc_step_kernel<32>, grid, dim3(kScBlock), 0, s, a); break;
+  }
   if (int rc = check_launch("sc_step_kernel")) return rc;
   if (autoreset) {
     st->time_step = 0;

@@ -18,6 +18,9 @@
 
 namespace scg {
 
+// Compile-time destination bound used for a chain whose widest node ships to d nodes.
+__host__ __device__ constexpr int sc_maxd_bucket(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32; }
+
 // Launch-uniform view of the configuration.
 struct ScCtx {
   const scg_sc_node* nodes;
@@ -124,27 +127,41 @@ __host__ __device__ inline void sc_reset_env(const ScCtx& c, ScEnv& e) {
 
 // SC_Action.apply for SHIP (:58-96): the cut [0, limit] split at the destinations'
 // sorted action values; amount_i = (v_(k) - v_(k-1)) * limit, clamped to what is left.
-__host__ __device__ inline void sc_split(const Num* vals, int D, Num limit, Num* out) {
-  for (int i = 0; i < D; ++i) out[i] = pyint(0);
+// Sorting (value, index) tuples is done by ranks so every array index is a compile-time
+// constant (MAXD-unrolled loops): the arrays stay in registers instead of scratch.
+template <int MAXD>
+__host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num limit, Num (&out)[MAXD]) {
+#pragma unroll
+  for (int i = 0; i < MAXD; ++i) out[i] = pyint(0);
   Num left = limit;
   if (!np_lt(pyint(0), left)) return;
-  int order[SCG_SC_MAX_DESTS];
-  for (int i = 0; i < D; ++i) {  // stable insertion sort on (value, index)
-    int j = i;
-    while (j > 0 && np_lt(vals[i], vals[order[j - 1]])) {
-      order[j] = order[j - 1];
-      --j;
-    }
-    order[j] = i;
+  int rank[MAXD];
+#pragma unroll
+  for (int i = 0; i < MAXD; ++i) {
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j)
+      if (j < D && (vals[j] < vals[i] || (vals[j] == vals[i] && j < i))) ++r;
+    rank[i] = r;
   }
-  Num prev = pyint(0);
-  for (int s = 0; s < D; ++s) {
-    const int i = order[s];
-    Num amt = np_mul(np_sub(vals[i], prev), limit);
+  float prev = 0.0f;
+  bool first = true;  // the first cut starts at the Python int 0
+#pragma unroll
+  for (int s = 0; s < MAXD; ++s) {
+    if (s >= D) break;
+    float v = 0.0f;
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i)
+      if (i < D && rank[i] == s) v = vals[i];
+    const Num diff = first ? np_sub(Num{v, NK_F32}, pyint(0)) : np_sub(Num{v, NK_F32}, Num{prev, NK_F32});
+    Num amt = np_mul(diff, limit);
     if (np_lt(left, amt)) amt = left;
-    out[i] = amt;
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i)
+      if (i < D && rank[i] == s) out[i] = amt;
     left = np_sub(left, amt);
-    prev = vals[i];
+    prev = v;
+    first = false;
   }
 }
 
@@ -155,7 +172,8 @@ __host__ __device__ __forceinline__ Num sc_action(const float* raw, int k) {
 }
 
 // SC_Node.act (:208-396) for node `ni` at time t; `act` = this env's raw float32 action
-// row. Returns the node's cost with its NumPy kind.
+// row. Returns the node's cost with its NumPy kind. MAXD bounds the node's destinations.
+template <int MAXD>
 __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& ltc, WordCache& dmc, int ni,
                                            const float* act, int t) {
   const scg_sc_node& nd = c.nodes[ni];
@@ -196,8 +214,9 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
   if (!nd.last_level) {
     // SHIP (:262-375)
     const int D = nd.n_dests;
-    Num ship_left[SCG_SC_MAX_DESTS];
-    for (int i = 0; i < D; ++i) ship_left[i] = pyint(nd.ship_capacity[i]);
+    Num ship_left[MAXD];
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) ship_left[i] = pyint(i < D ? nd.ship_capacity[i] : 0);
     Num proc_left = pyint(nd.processing_capacity);
     const int lt_base = lt_i;
     for (int p = 0; p < P; ++p) {
@@ -205,12 +224,17 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
       Num over_ship = pyint(0), over_proc = pyint(0);
       const Num material = f64(sc_stock(c, e, ni, p));
       if (np_lt(pyint(0), material)) {
-        Num vals[SCG_SC_MAX_DESTS], out[SCG_SC_MAX_DESTS], sent[SCG_SC_MAX_DESTS];
-        for (int i = 0; i < D; ++i) vals[i] = sc_action(act, nd.action_offset + a_i + i);
-        sc_split(vals, D, py_min(pyint(nd.stock_capacity[p]), material), out);
-        for (int i = 0; i < D; ++i) sent[i] = out[i];
+        float vals[MAXD];
+        Num out[MAXD], sent[MAXD];
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) vals[i] = i < D ? static_cast<float>(sc_action(act, nd.action_offset + a_i + i).v) : 0.0f;
+        sc_split<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), out);
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) sent[i] = out[i];
         if (nd.processing_capacity > 0) {  // factory: processing capacity and ratio (:298-310)
-          for (int i = 0; i < D; ++i) {
+#pragma unroll
+          for (int i = 0; i < MAXD; ++i) {
+            if (i >= D) break;
             if (np_lt(pyint(0), out[i])) {
               if (np_lt(proc_left, out[i])) {
                 over_proc = np_add(over_proc, np_sub(out[i], proc_left));
@@ -221,7 +245,9 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
             sent[i] = np_div(out[i], pyint(nd.processing_ratio[p]));
           }
         }
-        for (int i = 0; i < D; ++i) {  // per-destination ship capacity (:312-328)
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {  // per-destination ship capacity (:312-328)
+          if (i >= D) break;
           const Num amt = sent[i];
           if (np_lt(pyint(0), amt) && np_lt(ship_left[i], amt)) {
             over_ship = np_add(over_ship, np_sub(amt, ship_left[i]));
@@ -231,17 +257,20 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
           }
         }
         Num leaving = pyint(0);  // sum(amounts) (:331)
-        for (int i = 0; i < D; ++i) leaving = np_add(leaving, out[i]);
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i)
+          if (i < D) leaving = np_add(leaving, out[i]);
         double& st = sc_stock(c, e, ni, p);
         st = st - leaving.v;  // float64 array element minus the promoted scalar (:332)
         if (nd.processing_capacity > 0) cost = np_add(cost, np_mul(leaving, pyint(nd.processing_cost[p])));
-        int lt_k = lt_base;
-        for (int i = 0; i < D; ++i) {  // (:344-348)
-          if (np_lt(pyint(0), sent[i])) sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_k), sent[i]);
-          ++lt_k;
-        }
         Num ship_cost = pyint(0);  // sum(calculate_costs(amounts_to_ship)) (:352)
-        for (int i = 0; i < D; ++i) ship_cost = np_add(ship_cost, np_mul(sent[i], pyint(nd.dest_costs[p][i])));
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {  // (:344-348)
+          if (i >= D) break;
+          if (np_lt(pyint(0), sent[i]))
+            sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), sent[i]);
+          ship_cost = np_add(ship_cost, np_mul(sent[i], pyint(nd.dest_costs[p][i])));
+        }
         cost = np_add(cost, ship_cost);
       }
       cost = np_add(cost, np_mul(pyint(c.pen_proc), over_proc));  // :361
@@ -264,11 +293,12 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
 }
 
 // SupplyChainEnv.step body (:704-738) for time t (already incremented). Actions are the
-// raw float32 row in [-1, 1]; returns the reward.
+// raw float32 row in [-1, 1]; returns the reward. MAXD >= every node's destinations.
+template <int MAXD>
 __host__ __device__ inline double sc_step_env(const ScCtx& c, ScEnv& e, const float* act, int t) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   Num total = pyint(0);
-  for (int i = 0; i < c.n_nodes; ++i) total = np_add(total, sc_node_act(c, e, ltc, dmc, i, act, t));
+  for (int i = 0; i < c.n_nodes; ++i) total = np_add(total, sc_node_act<MAXD>(c, e, ltc, dmc, i, act, t));
   return np_neg(total).v;
 }
 

@@ -117,7 +117,7 @@ class ScConfig(ctypes.Structure):
         "n_nodes", "n_products", "n_retailers", "n_actions", "n_obs", "n_leadtimes", "total_time_steps",
         "avg_leadtime", "max_leadtime", "stochastic_leadtimes", "demand_lo", "demand_hi", "unmet_demand_cost",
         "exceeded_stock_capacity_cost", "exceeded_process_capacity_cost", "exceeded_ship_capacity_cost",
-        "heap_capacity", "leadtime_poisson_len", "obs_f64", "reserved")] + [
+        "heap_capacity", "leadtime_poisson_len", "obs_f64", "max_dests")] + [
         ("nodes", ctypes.c_void_p), ("leadtime_poisson", ctypes.c_void_p), ("demand_table", ctypes.c_void_p),
         ("leadtime_table", ctypes.c_void_p)]
 

@@ -248,7 +248,7 @@ typedef struct scg_sc_config {
   int32_t heap_capacity;        /* H: entries per (node, product) heap (scg_sc_prepare)    */
   int32_t leadtime_poisson_len;
   int32_t obs_f64;              /* observation dtype: 0 float32, 1 float64                 */
-  int32_t reserved;
+  int32_t max_dests;            /* out of scg_sc_prepare: most destinations of any node    */
   const scg_sc_node* nodes;     /* DEVICE [n_nodes]                                        */
   const uint32_t* leadtime_poisson; /* DEVICE Poisson(avg_leadtime-1) thresholds           */
   const int32_t* demand_table;  /* DEVICE [N][T+1][R][P] caller tables instead of Philox    */
@@ -276,7 +276,7 @@ typedef struct scg_sc_state {
 SCG_API int scg_sc_struct_sizes(size_t* node_size, size_t* config_size, size_t* state_size);
 
 /* Validate cfg against the host copy of the node table; fills n_actions, n_obs,
- * n_leadtimes and heap_capacity. Host only. */
+ * n_leadtimes, heap_capacity and max_dests. Host only. */
 SCG_API int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* host_nodes);
 
 /* reset() for all envs (:630-682). obs: DEVICE [N][n_obs] (float32 or float64) or NULL. */

@@ -57,7 +57,14 @@ extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, c
     std::memcpy(heap_size + t * NP, heap_size + (t - 1) * NP, sizeof(int32_t) * NP);
     scg::ScEnv et{stock + t * NP, heap_tk + static_cast<int64_t>(t) * NP * c.H,
                   heap_val + static_cast<int64_t>(t) * NP * c.H, heap_size + t * NP, 1, env_id, 0, episode, 0};
-    rewards[t - 1] = scg::sc_step_env(c, et, actions + static_cast<int64_t>(t - 1) * c.A, t);
+    const float* a = actions + static_cast<int64_t>(t - 1) * c.A;
+    switch (scg::sc_maxd_bucket(cfg->max_dests)) {  // the instantiation the GPU launch picks
+      case 2: rewards[t - 1] = scg::sc_step_env<2>(c, et, a, t); break;
+      case 4: rewards[t - 1] = scg::sc_step_env<4>(c, et, a, t); break;
+      case 8: rewards[t - 1] = scg::sc_step_env<8>(c, et, a, t); break;
+      case 16: rewards[t - 1] = scg::sc_step_env<16>(c, et, a, t); break;
+      default: rewards[t - 1] = scg::sc_step_env<32>(c, et, a, t); break;
+    }
     auto out = sink(obs + static_cast<int64_t>(t) * c.O);
     scg::sc_observe(c, et, t, out);
     if (et.overflow) return 1;
