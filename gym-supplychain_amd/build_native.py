@@ -25,7 +25,31 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+def build_binding(verbose=True):
+    """_scgpu_fast: METH_FASTCALL CPython binding of the per-step entry points."""
+    import sysconfig
+    src = os.path.join(CSRC, "scg_pybind.c")
+    out = os.path.join(HERE, "gym_supplychain_amd", "_scgpu_fast" + sysconfig.get_config_var("EXT_SUFFIX"))
+    deps = [src, OUT, os.path.join(REPO, "include", "scgpu.h")]
+    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-I", sysconfig.get_paths()["include"],
+           "-I", os.path.join(REPO, "include"), src, "-L", os.path.dirname(OUT), "-lscgpu",
+           "-Wl,-rpath,$ORIGIN", "-o", out + ".tmp"]
+    if verbose:
+        print("[build_native]", " ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build(debug=False, verbose=True):
+    lib = build_library(debug, verbose)
+    build_binding(verbose)
+    return lib
+
+
+def build_library(debug=False, verbose=True):
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
         [os.path.join(REPO, "include", "scgpu.h")]

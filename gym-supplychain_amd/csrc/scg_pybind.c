@@ -1,0 +1,87 @@
+/*
+ * _scgpu_fast: a METH_FASTCALL CPython binding of the per-step C-ABI entry points
+ * (scg_bg_step, scg_sc_step) so a Python step loop pays ~0.2 us of call overhead
+ * instead of ctypes' argument marshalling. It links libscgpu.so (the C ABI of
+ * include/scgpu.h) and adds no logic: arguments are the integer addresses of the
+ * ctypes config/state structs and the tensors' data_ptr()s.
+ *
+ * Return value: (status << 1) | done; status != 0 is turned into the mapped Python
+ * exception by the caller (gym_supplychain_amd._native.check).
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <stdint.h>
+
+#include "scgpu.h"
+
+static int as_ptr(PyObject* o, void** out) {
+  if (o == Py_None) {
+    *out = NULL;
+    return 0;
+  }
+  unsigned long long v = PyLong_AsUnsignedLongLong(o);
+  if (v == (unsigned long long)-1 && PyErr_Occurred()) return -1;
+  *out = (void*)(uintptr_t)v;
+  return 0;
+}
+
+/* bg_step(cfg, state, action, obs, reward, terminal_obs, flags, stream) */
+static PyObject* bg_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  void* p[8];
+  if (nargs != 8) {
+    PyErr_SetString(PyExc_TypeError, "bg_step expects 8 arguments");
+    return NULL;
+  }
+  for (int i = 0; i < 8; ++i)
+    if (as_ptr(args[i], &p[i])) return NULL;
+  int32_t done = 0;
+  const int rc = scg_bg_step((const scg_bg_config*)p[0], (scg_bg_state*)p[1], (const int32_t*)p[2], (int32_t*)p[3],
+                             (int32_t*)p[4], (int32_t*)p[5], (uint32_t)(uintptr_t)p[6], &done, p[7]);
+  return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
+}
+
+/* bg_step_timed(cfg, state, action, obs, reward, terminal_obs, flags, start_event, stop_event, stream) */
+static PyObject* bg_step_timed(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  void* p[10];
+  if (nargs != 10) {
+    PyErr_SetString(PyExc_TypeError, "bg_step_timed expects 10 arguments");
+    return NULL;
+  }
+  for (int i = 0; i < 10; ++i)
+    if (as_ptr(args[i], &p[i])) return NULL;
+  int32_t done = 0;
+  const int rc = scg_bg_step_timed((const scg_bg_config*)p[0], (scg_bg_state*)p[1], (const int32_t*)p[2],
+                                   (int32_t*)p[3], (int32_t*)p[4], (int32_t*)p[5], (uint32_t)(uintptr_t)p[6], &done,
+                                   p[7], p[8], p[9]);
+  return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
+}
+
+/* sc_step(cfg, state, action, obs, reward, terminal_obs, flags, stream) */
+static PyObject* sc_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  void* p[8];
+  if (nargs != 8) {
+    PyErr_SetString(PyExc_TypeError, "sc_step expects 8 arguments");
+    return NULL;
+  }
+  for (int i = 0; i < 8; ++i)
+    if (as_ptr(args[i], &p[i])) return NULL;
+  int32_t done = 0;
+  const int rc = scg_sc_step((const scg_sc_config*)p[0], (scg_sc_state*)p[1], (const float*)p[2], p[3],
+                             (double*)p[4], p[5], (uint32_t)(uintptr_t)p[6], &done, p[7]);
+  return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
+}
+
+static PyMethodDef methods[] = {
+    {"bg_step", (PyCFunction)(void (*)(void))bg_step, METH_FASTCALL, "scg_bg_step"},
+    {"bg_step_timed", (PyCFunction)(void (*)(void))bg_step_timed, METH_FASTCALL, "scg_bg_step_timed"},
+    {"sc_step", (PyCFunction)(void (*)(void))sc_step, METH_FASTCALL, "scg_sc_step"},
+    {NULL, NULL, 0, NULL},
+};
+
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_scgpu_fast", NULL, -1, methods,
+                                    NULL, NULL, NULL, NULL};
+
+PyMODINIT_FUNC PyInit__scgpu_fast(void) { return PyModule_Create(&module); }

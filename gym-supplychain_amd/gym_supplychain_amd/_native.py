@@ -196,6 +196,11 @@ def _load():
 
 lib = _load()
 
+try:  # METH_FASTCALL binding of the per-step entry points (links this same libscgpu.so)
+    from . import _scgpu_fast as fast
+except ImportError as exc:  # pragma: no cover - built together with libscgpu.so
+    raise NativeLibraryError(f"_scgpu_fast binding missing next to {LIB_PATH}: rebuild ({exc})")
+
 
 def last_error():
     msg = lib.scg_last_error()

@@ -213,8 +213,8 @@ class BeerGameVecEnv:
         self._act_shape = (n_envs, L)
         self._obs_ptr, self._rew_ptr = self._obs.data_ptr(), self._rew.data_ptr()
         self._term_ptr = self._term_obs.data_ptr()
-        self._step_fn = nat.lib.scg_bg_step
-        self._step_timed_fn = nat.lib.scg_bg_step_timed
+        self._cfg_addr, self._st_addr = ctypes.addressof(self._cfg), ctypes.addressof(self._st)
+        self._fast_step, self._fast_step_timed = nat.fast.bg_step, nat.fast.bg_step_timed
         # gym surface (an extension: the reference leaves both spaces unset, :62-64)
         self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
         self.single_action_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
@@ -251,15 +251,15 @@ class BeerGameVecEnv:
         if not self._is_ready(actions):
             actions = self._actions(actions)
         if _events is None:
-            rc = self._step_fn(self._cfg_ref, self._st_ref, actions.data_ptr(), self._obs_ptr, self._rew_ptr,
-                               self._term_ptr, self._flags, self._done_ref, nat.raw_stream(self._dev_index))
+            r = self._fast_step(self._cfg_addr, self._st_addr, actions.data_ptr(), self._obs_ptr, self._rew_ptr,
+                                self._term_ptr, self._flags, nat.raw_stream(self._dev_index))
         else:  # (start, stop) hipEvent_t handles stamped with the kernel's own dispatch times
-            rc = self._step_timed_fn(self._cfg_ref, self._st_ref, actions.data_ptr(), self._obs_ptr, self._rew_ptr,
-                                     self._term_ptr, self._flags, self._done_ref, _events[0], _events[1],
-                                     nat.raw_stream(self._dev_index))
-        if rc:
-            nat.check(rc)
-        if self._done_flag.value:
+            r = self._fast_step_timed(self._cfg_addr, self._st_addr, actions.data_ptr(), self._obs_ptr,
+                                      self._rew_ptr, self._term_ptr, self._flags, _events[0], _events[1],
+                                      nat.raw_stream(self._dev_index))
+        if r > 1:
+            nat.check(r >> 1)
+        if r & 1:
             info = {"terminal_observation": self._term_obs}
             if self._final_ret is not None:
                 info["episode_return"] = self._final_ret

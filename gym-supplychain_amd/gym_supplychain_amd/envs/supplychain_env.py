@@ -298,6 +298,9 @@ class SupplyChainVecEnv:
         self._done_ref = ctypes.byref(self._done_flag)
         self._flags = nat.SCG_BG_AUTORESET if self.auto_reset else 0
         self._act_shape = (n_envs, c.n_actions)
+        self._cfg_addr, self._st_addr = ctypes.addressof(self._cfg), ctypes.addressof(self._st)
+        self._obs_ptr, self._rew_ptr, self._term_ptr = (self._obs.data_ptr(), self._rew.data_ptr(),
+                                                        self._term_obs.data_ptr())
         self.single_action_space = spaces.Box(-1.0, 1.0, (c.n_actions,), np.float32)          # :625
         self.single_observation_space = spaces.Box(-1.0, 1.0, (c.n_obs,), np.float32)         # :626
 
@@ -330,12 +333,11 @@ class SupplyChainVecEnv:
         if not (type(a) is torch.Tensor and a.dtype is torch.float32 and a.is_cuda and
                 a.get_device() == self._dev_index and a.shape == self._act_shape and a.is_contiguous()):
             a = self._actions(a)
-        rc = nat.lib.scg_sc_step(self._cfg_ref, self._st_ref, a.data_ptr(), self._obs.data_ptr(),
-                                 self._rew.data_ptr(), self._term_obs.data_ptr(), self._flags, self._done_ref,
-                                 self._stream())
-        if rc:
-            nat.check(rc)
-        if self._done_flag.value:
+        r = nat.fast.sc_step(self._cfg_addr, self._st_addr, a.data_ptr(), self._obs_ptr, self._rew_ptr,
+                             self._term_ptr, self._flags, nat.raw_stream(self._dev_index))
+        if r > 1:
+            nat.check(r >> 1)
+        if r & 1:
             self.check_errors()
             info = {"terminal_observation": self._term_obs}
             if self._final_ret is not None:
