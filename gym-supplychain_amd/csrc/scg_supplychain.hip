@@ -55,7 +55,7 @@ struct ObsRow {
 };
 
 __device__ __forceinline__ ScEnv env_view(const ScArgs& a, int64_t n, uint32_t episode) {
-  return ScEnv{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
+  return ScEnv{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, a.n, static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
 }
 
 __global__ __launch_bounds__(kScBlock) void sc_reset_kernel(const ScArgs a) {
@@ -102,6 +102,74 @@ __global__ __launch_bounds__(kScBlock) void sc_step_kernel(const ScArgs a) {
     }
   }
   if (e.overflow) atomicOr(a.err, 1);
+}
+
+// The same step with this block's 64 env heaps staged in LDS: heap pushes/pops/walks are
+// chains of dependent accesses, so they run at LDS latency instead of L2/HBM latency.
+// Layout [slot][lane] (lane fastest): any mix of per-lane heap positions is bank-conflict
+// free. Stock stays in HBM (a few accesses per node). Rows are staged in and out with
+// coalesced 64-lane transfers, copying only the live entries (< heap size) of each lane.
+template <int MAXD>
+__global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + lane;
+  const ScCtx& c = a.c;
+  const int NP = c.n_nodes * c.P;
+  const int slots = NP * c.H;
+  double* lval = reinterpret_cast<double*>(smem);
+  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
+  int32_t* lsize = ltk + static_cast<int64_t>(slots) * kScBlock;
+  const bool live = n < a.n;
+  if (live) {
+    for (int hp = 0; hp < NP; ++hp) {
+      const int32_t sz = a.size[hp * a.n + n];
+      lsize[hp * kScBlock + lane] = sz;
+      for (int j = 0; j < sz; ++j) {
+        const int64_t g = (static_cast<int64_t>(hp) * c.H + j) * a.n + n;
+        ltk[(hp * c.H + j) * kScBlock + lane] = a.tk[g];
+        lval[(hp * c.H + j) * kScBlock + lane] = a.val[g];
+      }
+    }
+  }
+  if (!live) return;  // no block-wide sync below: every lane only touches its own column
+  ScEnv e{a.stock + n, ltk + lane, lval + lane, lsize + lane, a.n, kScBlock,
+          static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
+  const double reward = sc_step_env<MAXD>(c, e, a.act + n * c.A, a.t);
+  a.rew[n] = reward;
+  const bool terminal = a.flags & 1;
+  if (a.ep_ret) {
+    const double r = a.ep_ret[n] + reward;
+    if (terminal && a.final_ret) a.final_ret[n] = r;
+    a.ep_ret[n] = (a.flags & 2) ? 0.0 : r;
+  }
+  if (a.flags & 2) {
+    if (a.term_obs) {
+      ObsRow tout{a.term_obs, n * c.O, a.obs_f64};
+      sc_observe(c, e, a.t, tout);
+    }
+    e.episode = a.episode + 1;
+    sc_reset_env(c, e);
+    ObsRow out{a.obs, n * c.O, a.obs_f64};
+    sc_observe(c, e, 0, out);
+  } else {
+    ObsRow out{a.obs, n * c.O, a.obs_f64};
+    sc_observe(c, e, a.t, out);
+    if (terminal && a.term_obs) {
+      ObsRow tout{a.term_obs, n * c.O, a.obs_f64};
+      sc_observe(c, e, a.t, tout);
+    }
+  }
+  if (e.overflow) atomicOr(a.err, 1);
+  for (int hp = 0; hp < NP; ++hp) {
+    const int32_t sz = lsize[hp * kScBlock + lane];
+    a.size[hp * a.n + n] = sz;
+    for (int j = 0; j < sz; ++j) {
+      const int64_t g = (static_cast<int64_t>(hp) * c.H + j) * a.n + n;
+      a.tk[g] = ltk[(hp * c.H + j) * kScBlock + lane];
+      a.val[g] = lval[(hp * c.H + j) * kScBlock + lane];
+    }
+  }
 }
 
 __global__ __launch_bounds__(kScBlock) void sc_tables_kernel(const ScArgs a, int32_t* __restrict__ demand,
@@ -183,6 +251,13 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
 
 dim3 sc_grid(int64_t n) { return dim3(static_cast<unsigned>((n + kScBlock - 1) / kScBlock)); }
 
+// LDS the staged step kernel needs per 64-env block; staged only while >= 2 blocks fit a CU.
+constexpr size_t kScLdsMax = 64 * 1024;
+size_t sc_lds_bytes(const scg_sc_config* cfg) {
+  const size_t NP = static_cast<size_t>(cfg->n_nodes) * cfg->n_products;
+  return kScBlock * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
+}
+
 }  // namespace
 }  // namespace scg
 
@@ -235,21 +310,38 @@ int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
     n_lt += (nd.n_supply > 0 ? P : 0) + nd.n_dests;
   }
   if (n_ret != cfg->n_retailers || n_ret < 1) return fail(SCG_ERR_INVALID, "retailer count mismatch");
-  // heap bound: pushes per step into (node, p) x (longest lead time + 1) + initial entries
-  std::vector<int> indeg(static_cast<size_t>(NN) * P, 0);
-  for (int i = 0; i < NN; ++i) {
-    const scg_sc_node& nd = nodes[i];
-    for (int p = 0; p < P; ++p) {
-      if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) indeg[i * P + p] += 1;
-      if (!nd.last_level)
-        for (int d = 0; d < nd.n_dests; ++d) indeg[nd.dests[d] * P + p] += 1;
-    }
-  }
+  // Heap capacity: the peak occupancy of every (node, product) heap when every possible
+  // push happens with the longest lead time, simulated in the step's node order (pops
+  // of a node happen after its upstream nodes pushed). Shorter lead times and skipped
+  // (non-positive) shipments only lower occupancy, so this bounds every run; the
+  // kernels still flag an overflow (error_flags bit 0) instead of writing past it.
   const int lmax = cfg->stochastic_leadtimes ? cfg->max_leadtime : cfg->avg_leadtime;
+  const int horizon = std::min(cfg->total_time_steps, 4 * (lmax + 2) + SCG_SC_MAX_INIT);
+  const int span = horizon + lmax + SCG_SC_MAX_INIT + 2;
+  std::vector<int> due(static_cast<size_t>(NN) * P * span, 0), occ(static_cast<size_t>(NN) * P, 0);
   int H = 1, maxd = 0;
   for (int i = 0; i < NN; ++i) maxd = std::max(maxd, nodes[i].n_dests);
   for (int i = 0; i < NN; ++i)
-    for (int p = 0; p < P; ++p) H = std::max(H, indeg[i * P + p] * (lmax + 1) + nodes[i].n_init[p]);
+    for (int p = 0; p < P; ++p)
+      for (int j = 0; j < nodes[i].n_init[p]; ++j) {
+        due[(static_cast<size_t>(i) * P + p) * span + nodes[i].init_time[p][j]] += 1;
+        H = std::max(H, ++occ[i * P + p]);
+      }
+  auto push = [&](int node, int p, int when) {
+    due[(static_cast<size_t>(node) * P + p) * span + when] += 1;
+    H = std::max(H, ++occ[node * P + p]);
+  };
+  for (int t = 1; t <= horizon; ++t)
+    for (int i = 0; i < NN; ++i) {
+      const scg_sc_node& nd = nodes[i];
+      for (int p = 0; p < P; ++p) occ[i * P + p] -= due[(static_cast<size_t>(i) * P + p) * span + t];
+      for (int p = 0; p < P; ++p)
+        if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) push(i, p, t + lmax);
+      if (!nd.last_level)
+        for (int p = 0; p < P; ++p)
+          if (nd.stock_capacity[p] > 0)
+            for (int d = 0; d < nd.n_dests; ++d) push(nd.dests[d], p, t + lmax);
+    }
   cfg->n_actions = n_act;
   cfg->n_leadtimes = n_lt;
   cfg->n_obs = n_ret * P + NN * P + NN * P * cfg->avg_leadtime + 1;
@@ -288,7 +380,16 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
   a.flags = (terminal ? 1 : 0) | (autoreset ? 2 : 0);
   const dim3 grid = sc_grid(st->n_envs);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (sc_maxd_bucket(cfg->max_dests)) {
+  const size_t lds = sc_lds_bytes(cfg);
+  if (lds <= kScLdsMax) {
+    switch (sc_maxd_bucket(cfg->max_dests)) {
+      case 2: hipLaunchKernelGGL(sc_step_lds_kernel<2>, grid, dim3(kScBlock), lds, s, a); break;
+      case 4: hipLaunchKernelGGL(sc_step_lds_kernel<4>, grid, dim3(kScBlock), lds, s, a); break;
+      case 8: hipLaunchKernelGGL(sc_step_lds_kernel<8>, grid, dim3(kScBlock), lds, s, a); break;
+      case 16: hipLaunchKernelGGL(sc_step_lds_kernel<16>, grid, dim3(kScBlock), lds, s, a); break;
+      default: hipLaunchKernelGGL(sc_step_lds_kernel<32>, grid, dim3(kScBlock), lds, s, a); break;
+    }
+  } else switch (sc_maxd_bucket(cfg->max_dests)) {
     case 2: hipLaunchKernelGGL(sc_step_kernel<2>, grid, dim3(kScBlock), 0, s, a); break;
     case 4: hipLaunchKernelGGL(sc_step_kernel<4>, grid, dim3(kScBlock), 0, s, a); break;
     case 8: hipLaunchKernelGGL(sc_step_kernel<8>, grid, dim3(kScBlock), 0, s, a); break;

@@ -34,13 +34,15 @@ struct ScCtx {
   uint32_t key0, key1;
 };
 
-// One env's state: element i of a per-env array lives at [i * stride].
+// One env's state: element i of a per-env array lives at [i * stride] (stock) or
+// [i * hstride] (heap arrays, which the LDS-staged kernel keeps in shared memory).
 struct ScEnv {
   double* stock;     // [NP]
   int32_t* tk;       // [NP][H]
   double* val;       // [NP][H]
   int32_t* size;     // [NP]
   int64_t stride;    // envs in the batch
+  int64_t hstride;   // heap-array stride: the batch (global) or the block (LDS)
   uint32_t env_id;   // global id (Philox counter)
   int64_t local;     // index in this shard (caller tables)
   uint32_t episode;
@@ -49,11 +51,11 @@ struct ScEnv {
 
 __host__ __device__ __forceinline__ HeapView sc_heap(const ScCtx& c, const ScEnv& e, int node, int p) {
   const int64_t hp = static_cast<int64_t>(node) * c.P + p;
-  return HeapView{e.tk + hp * c.H * e.stride, e.val + hp * c.H * e.stride, e.stride};
+  return HeapView{e.tk + hp * c.H * e.hstride, e.val + hp * c.H * e.hstride, e.hstride};
 }
 
 __host__ __device__ __forceinline__ int32_t& sc_size(const ScCtx& c, const ScEnv& e, int node, int p) {
-  return e.size[(static_cast<int64_t>(node) * c.P + p) * e.stride];
+  return e.size[(static_cast<int64_t>(node) * c.P + p) * e.hstride];
 }
 
 __host__ __device__ __forceinline__ double& sc_stock(const ScCtx& c, const ScEnv& e, int node, int p) {
@@ -148,7 +150,7 @@ __host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num l
   bool first = true;  // the first cut starts at the Python int 0
 #pragma unroll
   for (int s = 0; s < MAXD; ++s) {
-    if (s >= D) break;
+    if (s >= D) continue;
     float v = 0.0f;
 #pragma unroll
     for (int i = 0; i < MAXD; ++i)
@@ -234,22 +236,22 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         if (nd.processing_capacity > 0) {  // factory: processing capacity and ratio (:298-310)
 #pragma unroll
           for (int i = 0; i < MAXD; ++i) {
-            if (i >= D) break;
-            if (np_lt(pyint(0), out[i])) {
-              if (np_lt(proc_left, out[i])) {
-                over_proc = np_add(over_proc, np_sub(out[i], proc_left));
-                out[i] = proc_left;
+            if (i < D) {
+              if (np_lt(pyint(0), out[i])) {
+                if (np_lt(proc_left, out[i])) {
+                  over_proc = np_add(over_proc, np_sub(out[i], proc_left));
+                  out[i] = proc_left;
+                }
+                proc_left = np_sub(proc_left, out[i]);
               }
-              proc_left = np_sub(proc_left, out[i]);
+              sent[i] = np_div(out[i], pyint(nd.processing_ratio[p]));
             }
-            sent[i] = np_div(out[i], pyint(nd.processing_ratio[p]));
           }
         }
 #pragma unroll
         for (int i = 0; i < MAXD; ++i) {  // per-destination ship capacity (:312-328)
-          if (i >= D) break;
           const Num amt = sent[i];
-          if (np_lt(pyint(0), amt) && np_lt(ship_left[i], amt)) {
+          if (i < D && np_lt(pyint(0), amt) && np_lt(ship_left[i], amt)) {
             over_ship = np_add(over_ship, np_sub(amt, ship_left[i]));
             sent[i] = ship_left[i];
             out[i] = nd.processing_capacity > 0 ? np_mul(sent[i], pyint(nd.processing_ratio[p])) : sent[i];
@@ -266,10 +268,11 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         Num ship_cost = pyint(0);  // sum(calculate_costs(amounts_to_ship)) (:352)
 #pragma unroll
         for (int i = 0; i < MAXD; ++i) {  // (:344-348)
-          if (i >= D) break;
-          if (np_lt(pyint(0), sent[i]))
-            sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), sent[i]);
-          ship_cost = np_add(ship_cost, np_mul(sent[i], pyint(nd.dest_costs[p][i])));
+          if (i < D) {
+            if (np_lt(pyint(0), sent[i]))
+              sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), sent[i]);
+            ship_cost = np_add(ship_cost, np_mul(sent[i], pyint(nd.dest_costs[p][i])));
+          }
         }
         cost = np_add(cost, ship_cost);
       }

@@ -40,7 +40,7 @@ extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, c
   int32_t* tk = heap_tk;
   double* val = heap_val;
   int32_t* sz = heap_size;
-  scg::ScEnv e{st, tk, val, sz, 1, env_id, 0, episode, 0};
+  scg::ScEnv e{st, tk, val, sz, 1, 1, env_id, 0, episode, 0};
   scg::sc_reset_env(c, e);
   auto sink = [&](double* row) { return [row](int o, double x) { row[o] = x; }; };
   {
@@ -56,7 +56,7 @@ extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, c
                 sizeof(double) * NP * c.H);
     std::memcpy(heap_size + t * NP, heap_size + (t - 1) * NP, sizeof(int32_t) * NP);
     scg::ScEnv et{stock + t * NP, heap_tk + static_cast<int64_t>(t) * NP * c.H,
-                  heap_val + static_cast<int64_t>(t) * NP * c.H, heap_size + t * NP, 1, env_id, 0, episode, 0};
+                  heap_val + static_cast<int64_t>(t) * NP * c.H, heap_size + t * NP, 1, 1, env_id, 0, episode, 0};
     const float* a = actions + static_cast<int64_t>(t - 1) * c.A;
     switch (scg::sc_maxd_bucket(cfg->max_dests)) {  // the instantiation the GPU launch picks
       case 2: rewards[t - 1] = scg::sc_step_env<2>(c, et, a, t); break;
