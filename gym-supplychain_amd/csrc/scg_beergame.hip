@@ -276,19 +276,42 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const W
   if (a.ep_ret) a.ep_ret[n] = ret;
 }
 
-// K weeks per launch, inventory/backlog/orders/ledgers/return in registers; only the
-// pipeline ring (read-modify-write through L2), actions in and obs/rewards out touch
-// memory per week.
 struct RolloutWeeks {
   WeekInfo wk[SCG_BG_ROLLOUT_MAX];
 };
 
+// Pipeline ring views for the rollout kernel: rows in HBM ([slot][N][L], the state
+// layout) or staged in LDS for the whole launch ([slot*L + l][lane], lane fastest, so
+// per-lane slot choices never conflict on banks).
 template <int L>
-__global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int32_t K, const RolloutWeeks weeks,
-                                                            const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
-                                                            int32_t* __restrict__ rew_out) {
-  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (n >= a.n) return;
+struct RingHbm {
+  int32_t* base;
+  int64_t stride, row;
+  __device__ __forceinline__ void load(int s, int32_t (&v)[L]) const { load_row<L>(base + s * stride + row, v); }
+  __device__ __forceinline__ void store(int s, const int32_t (&v)[L]) const { store_row<L>(base + s * stride + row, v); }
+};
+
+template <int L>
+struct RingLds {
+  int32_t* base;  // LDS + lane
+  __device__ __forceinline__ void load(int s, int32_t (&v)[L]) const {
+#pragma unroll
+    for (int l = 0; l < L; ++l) v[l] = base[(s * L + l) * kBlock];
+  }
+  __device__ __forceinline__ void store(int s, const int32_t (&v)[L]) const {
+#pragma unroll
+    for (int l = 0; l < L; ++l) base[(s * L + l) * kBlock] = v[l];
+  }
+};
+
+// K weeks per launch, inventory/backlog/orders/ledgers/return in registers; per week only
+// the action row in and the obs/reward (and history) rows out touch HBM. With LDS the
+// pipeline ring is staged in shared memory for the whole launch (loaded once, stored
+// once); otherwise its rows are read-modify-written through L2.
+template <int L, class Ring>
+__device__ __forceinline__ void rollout_body(const BgArgs& a, int64_t n, int32_t K, const RolloutWeeks& weeks,
+                                             const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
+                                             int32_t* __restrict__ rew_out, const Ring& ring) {
   const int64_t row = n * L;
   const int64_t stride = a.n * L;
   int32_t inv[L], bk[L], op[L], iacc[L], bacc[L];
@@ -306,17 +329,17 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int3
     int32_t act[L], due[L], obs[L], ic[L], bc[L], ship[L];
     load_row<L>(acts + k * stride + row, act);
     zero_row<L>(due);
-    if (wk.read_slot >= 0) load_row<L>(a.ring + wk.read_slot * stride + row, due);
+    if (wk.read_slot >= 0) ring.load(wk.read_slot, due);
     const int32_t demand = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, episode);
     const int32_t reward = step_core<L>(a.h, a.b, demand, wk.mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
     if (wk.mode == MODE_STORE) {
-      store_row<L>(a.ring + wk.write_slot * stride + row, ship);
+      ring.store(wk.write_slot, ship);
     } else if (wk.mode == MODE_ADD) {
       int32_t cur[L];
-      load_row<L>(a.ring + wk.write_slot * stride + row, cur);
+      ring.load(wk.write_slot, cur);
 #pragma unroll
       for (int l = 0; l < L; ++l) cur[l] += ship[l];
-      store_row<L>(a.ring + wk.write_slot * stride + row, cur);
+      ring.store(wk.write_slot, cur);
     }
     if (a.hist) store_row<L>(a.hist + static_cast<int64_t>(wk.week) * stride + row, op);
     ret += reward;
@@ -335,7 +358,10 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int3
         iacc[l] = bacc[l] = 0;
         obs[l] = inv[l];
       }
-      for (int t = 1; t <= a.init_slots; ++t) fill_row<L>(a.ring + (t % a.ring_slots) * stride + row, a.ship_value);
+      int32_t init[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) init[l] = a.ship_value;
+      for (int t = 1; t <= a.init_slots; ++t) ring.store(t % a.ring_slots, init);
       if (a.hist) fill_row<L>(a.hist + row, a.orders_value);
       ret = 0;
       ++episode;
@@ -349,6 +375,38 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int3
   if (a.inv_acc) store_row<L>(a.inv_acc + row, iacc);
   if (a.bk_acc) store_row<L>(a.bk_acc + row, bacc);
   if (a.ep_ret) a.ep_ret[n] = ret;
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int32_t K, const RolloutWeeks weeks,
+                                                            const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
+                                                            int32_t* __restrict__ rew_out) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= a.n) return;
+  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, RingHbm<L>{a.ring, a.n * L, n * L});
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void bg_rollout_lds_kernel(const BgArgs a, int32_t K, const RolloutWeeks weeks,
+                                                                const int32_t* __restrict__ acts,
+                                                                int32_t* __restrict__ obs_out,
+                                                                int32_t* __restrict__ rew_out) {
+  extern __shared__ int32_t lds_ring[];
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= a.n) return;  // lanes only touch their own LDS column: no block barrier needed
+  const RingHbm<L> hbm{a.ring, a.n * L, n * L};
+  const RingLds<L> lds{lds_ring + threadIdx.x};
+  for (int s = 0; s < a.ring_slots; ++s) {
+    int32_t v[L];
+    hbm.load(s, v);
+    lds.store(s, v);
+  }
+  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, lds);
+  for (int s = 0; s < a.ring_slots; ++s) {
+    int32_t v[L];
+    lds.load(s, v);
+    hbm.store(s, v);
+  }
 }
 
 // Philox draws for tests/benchmarks ------------------------------------------------------
@@ -410,6 +468,16 @@ int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo
 
 int launch_rollout(int L, dim3 grid, hipStream_t s, const BgArgs& a, int32_t K, const RolloutWeeks& weeks,
                    const int32_t* acts, int32_t* obs, int32_t* rew) {
+  const size_t lds = static_cast<size_t>(a.ring_slots) * L * kBlock * sizeof(int32_t);
+  if (lds <= 64 * 1024) {  // ring staged in LDS for the launch
+    switch (L) {
+#define X(l) case l: hipLaunchKernelGGL(bg_rollout_lds_kernel<l>, grid, dim3(kBlock), lds, s, a, K, weeks, acts, obs, rew); break;
+      SCG_LEVEL_CASES(X)
+#undef X
+      default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
+    }
+    return check_launch("bg_rollout_lds_kernel");
+  }
   switch (L) {
 #define X(l) case l: hipLaunchKernelGGL(bg_rollout_kernel<l>, grid, dim3(kBlock), 0, s, a, K, weeks, acts, obs, rew); break;
     SCG_LEVEL_CASES(X)
