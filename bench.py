@@ -63,6 +63,25 @@ def step_bytes_per_env(plan_word, week, T, L, ring_initial_slots, ledgers, histo
     return b
 
 
+def pmc_traffic(kernel_substr="bg_step_kernel<4>", n_envs=N_ENVS):
+    """HBM bytes per launch of the step kernel from the latest committed PMC summary
+    (profiles/rNN_pmc_summary.json, written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench at 65,536 envs; FETCH_SIZE
+    doubled per MI355X_MICROARCH.md §HBM). None when absent or for another batch size."""
+    import glob
+    if n_envs != N_ENVS:
+        return None, None
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        traffic = json.load(f).get("traffic", {})
+    for name, t in traffic.items():
+        if kernel_substr in name and t.get("hbm_bytes_per_launch"):
+            return t["hbm_bytes_per_launch"], os.path.relpath(files[-1], REPO)
+    return None, None
+
+
 def cpu_baseline(budget_s=1.5, max_procs=16):
     """Per-env NumPy restatement of BeerGameEnv.step on the host's cores (oracle, 'port')."""
     import multiprocessing as mp
@@ -187,6 +206,7 @@ def main():
         value = N * world * args.steps / elapsed
         avg_kernel_s = kern_ms / 1e3 / args.steps
         achieved = total_bytes / args.steps / avg_kernel_s / 1e9
+        traffic, traffic_src = pmc_traffic(n_envs=N)
         line = {
             "metric": "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X",
             "value": value,
@@ -205,7 +225,7 @@ def main():
                        "ledgers": True, "orders_history": True, "episode_return_allgather": world > 1,
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "scg::bg_step_kernel<4>", "avg_kernel_us": avg_kernel_s * 1e6,
                          "bytes_per_launch": total_bytes / args.steps},
         }
