@@ -66,6 +66,11 @@ struct BgArgs {
   int32_t init_slots;  // weeks 1..init_slots hold the initial pipeline (:52)
   int32_t ring_slots;
   int32_t init_inv[SCG_BG_MAX_LEVELS];
+  // BeerGameEnv2 (beergame2_env.py)
+  int32_t* pen_acc;    // penalty_costs ledger (:184)
+  int32_t max_stock, penalty;
+  int32_t demand_lo, demand_hi;
+  int32_t stochastic_delays, delay_lo, delay_hi, max_weeks;
 };
 
 // ---- row helpers: L contiguous int32 per env, widest aligned vector access ----------
@@ -118,6 +123,11 @@ __device__ __forceinline__ void fill_row(int32_t* __restrict__ p, int32_t x) {
 __device__ __forceinline__ int32_t week_demand(const BgArgs& a, int64_t n, int32_t week,
                                                uint32_t episode) {
   if (a.demand_mode == SCG_DEMAND_TABLE) return a.demand_table[(int64_t)(week - 1) * a.n + n];
+  if (a.demand_mode == SCG_DEMAND_UNIFORM) {  // randint(lo, hi), hi exclusive (beergame2_env.py:76-77)
+    const uint32_t w = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), episode,
+                                        static_cast<uint32_t>(week - 1), SCG_STREAM_BG2_DEMAND);
+    return a.demand_lo + static_cast<int32_t>((static_cast<uint64_t>(w) * static_cast<uint32_t>(a.demand_hi - a.demand_lo)) >> 32);
+  }
   const uint32_t u = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n),
                                       episode, static_cast<uint32_t>(week - 1), SCG_STREAM_DEMAND);
   // Inverse CDF on uint32 thresholds: #{k : thr[k] <= u}. The index is wave-uniform, so
@@ -139,12 +149,19 @@ __device__ __forceinline__ void reset_env(const BgArgs& a, int64_t n, int32_t* _
   store_row<L>(a.inv + row, inv);
   fill_row<L>(a.bk + row, 0);
   fill_row<L>(a.op + row, a.orders_value);
+  if (a.stochastic_delays)  // per-lane delays read-modify-write every slot: start clean
+    for (int s = 0; s < a.ring_slots; ++s) fill_row<L>(a.ring + s * stride + row, 0);
   for (int t = 1; t <= a.init_slots; ++t) fill_row<L>(a.ring + (t % a.ring_slots) * stride + row, a.ship_value);
   if (a.inv_acc) fill_row<L>(a.inv_acc + row, 0);
   if (a.bk_acc) fill_row<L>(a.bk_acc + row, 0);
+  if (a.pen_acc) fill_row<L>(a.pen_acc + row, 0);
   if (a.hist) fill_row<L>(a.hist + row, a.orders_value);  // all_orders_placed[:, 0] (:152)
   if (a.ep_ret) a.ep_ret[n] = 0;
-  if (obs_out) store_row<L>(obs_out + row, inv);            // inventory - backlog, backlog = 0
+  if (obs_out) {  // inventory - backlog with backlog = 0 (v2: + max_stock, beergame2_env.py:112)
+#pragma unroll
+    for (int l = 0; l < L; ++l) inv[l] += a.max_stock;
+    store_row<L>(obs_out + row, inv);
+  }
 }
 
 template <int L>
@@ -273,6 +290,106 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const W
     for (int l = 0; l < L; ++l) bacc[l] += bc[l];
     store_row<L>(a.bk_acc + row, bacc);
   }
+  if (a.ep_ret) a.ep_ret[n] = ret;
+}
+
+// BeerGameEnv2.step (beergame2_env.py:114-192): the v1 week with absolute orders
+// (:168), the observation offset by max_stock (:112), a penalty on stock and backlog
+// beyond max_stock (:179-180, :184), and optionally per-episode random shipment delays
+// (:90-92): then each lane draws its own delay, the due ring slot is cleared after it is
+// received and the scheduled slot is always read-modify-written (no shared week plan).
+template <int L>
+__global__ __launch_bounds__(kBlock) void bg2_step_kernel(const BgArgs a, const WeekInfo wk) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= a.n) return;
+  const int64_t row = n * L;
+  const int64_t stride = a.n * L;
+  const bool terminal = wk.flags & 1;
+  const bool autoreset = wk.flags & 2;
+  int32_t read_slot = wk.read_slot, write_slot = wk.write_slot, mode = wk.mode;
+  if (a.stochastic_delays) {
+    const uint32_t u = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), a.episode,
+                                        static_cast<uint32_t>(wk.week - 1), SCG_STREAM_BG2_DELAY);
+    const int32_t d = a.delay_lo + static_cast<int32_t>((static_cast<uint64_t>(u) * static_cast<uint32_t>(a.delay_hi - a.delay_lo)) >> 32);
+    read_slot = wk.week % a.ring_slots;
+    write_slot = (wk.week + d) % a.ring_slots;
+    mode = d == 0 ? MODE_DIRECT : (wk.week + d > a.max_weeks ? MODE_DROP : MODE_ADD);
+  }
+  int32_t inv[L], bk[L], op[L], act[L], due[L], cur[L], iacc[L], bacc[L], pacc[L];
+  load_row<L>(a.inv + row, inv);
+  load_row<L>(a.bk + row, bk);
+  load_row<L>(a.op + row, op);
+  load_row<L>(a.act + row, act);
+  zero_row<L>(due);
+  zero_row<L>(cur);
+  zero_row<L>(iacc);
+  zero_row<L>(bacc);
+  zero_row<L>(pacc);
+  if (read_slot >= 0) load_row<L>(a.ring + read_slot * stride + row, due);
+  if (mode == MODE_ADD) load_row<L>(a.ring + write_slot * stride + row, cur);
+  if (!autoreset && a.inv_acc) load_row<L>(a.inv_acc + row, iacc);
+  if (!autoreset && a.bk_acc) load_row<L>(a.bk_acc + row, bacc);
+  if (!autoreset && a.pen_acc) load_row<L>(a.pen_acc + row, pacc);
+  const int64_t ret0 = a.ep_ret ? a.ep_ret[n] : 0;
+  const int32_t demand = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, a.episode);
+
+  int32_t inc[L], fill[L], del[L], ship[L], obs[L];
+  inc[0] = demand;
+#pragma unroll
+  for (int l = 1; l < L; ++l) inc[l] = op[l - 1];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    inv[l] += due[l];
+    fill[l] = inc[l] + bk[l];
+    del[l] = min(inv[l], fill[l]);
+  }
+#pragma unroll
+  for (int l = 0; l + 1 < L; ++l) ship[l] = del[l + 1];
+  ship[L - 1] = op[L - 1];
+  int32_t cost = 0, pen = 0;
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    inv[l] += (mode == MODE_DIRECT ? ship[l] : 0) - del[l];
+    bk[l] = fill[l] - del[l];
+    op[l] = act[l];                                   // absolute orders (:168)
+    obs[l] = a.max_stock + inv[l] - bk[l];
+    const int32_t over = max(inv[l] - a.max_stock, 0) + max(bk[l] - a.max_stock, 0);
+    iacc[l] += a.h * inv[l];
+    bacc[l] += a.b * bk[l];
+    pacc[l] += a.penalty * over;
+    cost += a.h * inv[l] + a.b * bk[l];
+    pen += a.penalty * over;
+  }
+  const int32_t reward = -cost - pen;                 // :177-180
+
+  if (a.stochastic_delays) {  // consumed: the slot is reused R weeks on
+    int32_t z[L];
+    zero_row<L>(z);
+    store_row<L>(a.ring + read_slot * stride + row, z);
+  }
+  if (mode == MODE_STORE) {
+    store_row<L>(a.ring + write_slot * stride + row, ship);
+  } else if (mode == MODE_ADD) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) cur[l] += ship[l];
+    store_row<L>(a.ring + write_slot * stride + row, cur);
+  }
+  a.rew[n] = reward;
+  if (a.hist) store_row<L>(a.hist + static_cast<int64_t>(wk.week) * stride + row, op);
+  if (terminal && a.term_obs) store_row<L>(a.term_obs + row, obs);
+  const int64_t ret = ret0 + reward;
+  if (terminal && a.final_ret) a.final_ret[n] = ret;
+  if (autoreset) {
+    reset_env<L>(a, n, a.obs);
+    return;
+  }
+  store_row<L>(a.inv + row, inv);
+  store_row<L>(a.bk + row, bk);
+  store_row<L>(a.op + row, op);
+  store_row<L>(a.obs + row, obs);
+  if (a.inv_acc) store_row<L>(a.inv_acc + row, iacc);
+  if (a.bk_acc) store_row<L>(a.bk_acc + row, bacc);
+  if (a.pen_acc) store_row<L>(a.pen_acc + row, pacc);
   if (a.ep_ret) a.ep_ret[n] = ret;
 }
 
@@ -453,6 +570,16 @@ int launch_reset(int L, dim3 grid, hipStream_t s, const BgArgs& a) {
   return check_launch("bg_reset_kernel");
 }
 
+int launch_step2(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk) {
+  switch (L) {
+#define X(l) case l: hipLaunchKernelGGL(bg2_step_kernel<l>, grid, dim3(kBlock), 0, s, a, wk); break;
+    SCG_LEVEL_CASES(X)
+#undef X
+    default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
+  }
+  return check_launch("bg2_step_kernel");
+}
+
 int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk, hipEvent_t ev0,
                 hipEvent_t ev1) {
   // hipExtLaunchKernelGGL ties the optional events to this dispatch's own start/end
@@ -530,6 +657,17 @@ BgArgs make_args(const scg_bg_config* cfg, const scg_bg_state* st) {
   a.init_slots = std::min(cfg->shipment_delays ? cfg->shipment_delays[0] : 0, cfg->max_weeks);
   a.ring_slots = cfg->ring_slots;
   for (int l = 0; l < cfg->levels; ++l) a.init_inv[l] = cfg->initial_inventory[l];
+  a.demand_lo = cfg->demand_lo;
+  a.demand_hi = cfg->demand_hi;
+  a.max_weeks = cfg->max_weeks;
+  if (cfg->variant == 2) {
+    a.pen_acc = st->penalty_costs;
+    a.max_stock = cfg->max_stock;
+    a.penalty = cfg->exceeded_capacity_penalty;
+    a.stochastic_delays = cfg->stochastic_delays;
+    a.delay_lo = cfg->delay_lo;
+    a.delay_hi = cfg->delay_hi;
+  }
   return a;
 }
 
@@ -570,8 +708,14 @@ int scg_bg_prepare(scg_bg_config* cfg) {
   if (L < 1 || L > SCG_BG_MAX_LEVELS) return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
   if (T < 1 || T > SCG_BG_MAX_WEEKS) return fail(SCG_ERR_INVALID, "max_weeks=%d outside 1..%d", T, SCG_BG_MAX_WEEKS);
   if (!cfg->shipment_delays || !cfg->plan) return fail(SCG_ERR_INVALID, "shipment_delays and plan are required");
-  if (cfg->demand_mode < SCG_DEMAND_FIXED || cfg->demand_mode > SCG_DEMAND_POISSON)
+  if (cfg->variant == 0) cfg->variant = 1;
+  if (cfg->variant != 1 && cfg->variant != 2) return fail(SCG_ERR_INVALID, "variant must be 1 or 2");
+  if (cfg->demand_mode < SCG_DEMAND_FIXED || cfg->demand_mode > SCG_DEMAND_UNIFORM)
     return fail(SCG_ERR_INVALID, "unknown demand_mode %d", cfg->demand_mode);
+  if (cfg->demand_mode == SCG_DEMAND_UNIFORM && !(cfg->demand_hi > cfg->demand_lo))
+    return fail(SCG_ERR_INVALID, "uniform demand needs demand_lo < demand_hi");
+  if (cfg->variant == 1 && cfg->stochastic_delays)
+    return fail(SCG_ERR_INVALID, "stochastic shipment delays are a BeerGameEnv2 option");
   if (cfg->demand_mode == SCG_DEMAND_FIXED && !cfg->customer_demand)
     return fail(SCG_ERR_INVALID, "FIXED demand mode needs customer_demand");
   if (cfg->demand_mode == SCG_DEMAND_POISSON && (cfg->poisson_len < 1 || cfg->poisson_len > SCG_POISSON_MAX))
@@ -583,7 +727,12 @@ int scg_bg_prepare(scg_bg_config* cfg) {
       return fail(SCG_ERR_INVALID, "shipment_delays[%d]=%d outside 0..%d", w, d, SCG_BG_MAX_DELAY);
     max_delay = std::max(max_delay, d);
   }
-  const int32_t R = max_delay + 1;
+  int32_t R = max_delay + 1;
+  if (cfg->stochastic_delays) {  // per-lane randint(lo, hi) delays: ring covers hi - 1 and the initial 2
+    if (cfg->delay_lo < 0 || cfg->delay_hi <= cfg->delay_lo || cfg->delay_hi > SCG_BG_MAX_DELAY + 1)
+      return fail(SCG_ERR_INVALID, "stochastic delays need 0 <= delay_lo < delay_hi <= %d", SCG_BG_MAX_DELAY + 1);
+    R = std::max(R, cfg->delay_hi);
+  }
   // Which arrival weeks have been written, in week order (writes only target later weeks).
   std::vector<uint8_t> written(static_cast<size_t>(T) + 2, 0);
   const int32_t d0 = cfg->shipment_delays[0];
@@ -659,9 +808,12 @@ int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t*
   a.obs = obs;
   a.rew = reward;
   a.term_obs = terminal_obs;
-  if (int rc = launch_step(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a, wk,
-                           static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event)))
+  if (cfg->variant == 2) {
+    if (int rc = launch_step2(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a, wk)) return rc;
+  } else if (int rc = launch_step(cfg->levels, grid_for(st->n_envs), static_cast<hipStream_t>(stream), a, wk,
+                                  static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event))) {
     return rc;
+  }
   if (wk.flags & 2) {
     st->week = 0;
     st->episode += 1;
@@ -676,6 +828,7 @@ int scg_bg_rollout(const scg_bg_config* cfg, scg_bg_state* st, int32_t n_weeks, 
                    int32_t* obs, int32_t* rewards, uint32_t flags, void* stream) {
   if (int rc = check_state(cfg, st)) return rc;
   if (!actions || n_weeks < 0) return fail(SCG_ERR_INVALID, "rollout needs actions and n_weeks >= 0");
+  if (cfg->variant == 2) return fail(SCG_ERR_INVALID, "rollout is not implemented for BeerGameEnv2");
   if (int rc = check_step(cfg, st)) return rc;
   if (!(flags & SCG_BG_AUTORESET) && st->week + static_cast<int64_t>(n_weeks) > cfg->max_weeks)
     return fail(SCG_ERR_PAST_HORIZON, "rollout of %d weeks from week %d passes the terminal week %d", n_weeks,

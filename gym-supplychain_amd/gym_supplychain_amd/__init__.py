@@ -9,20 +9,21 @@ dynamics run as fused HIP kernels through the C ABI in include/scgpu.h.
     venv = gsa.make_vec("beergame-v0", 65536, demand="poisson", seed=0)   # batched
 """
 from . import _native  # noqa: F401  (fails loudly when libscgpu.so is missing)
-from .envs import (SCENARIOS, BeerGameEnv, BeerGameVecEnv, SupplyChain2perStageEnv, SupplyChainEnv,
+from .envs import (SCENARIOS, BeerGame2VecEnv, BeerGameEnv, BeerGameEnv2, BeerGameVecEnv, SupplyChain2perStageEnv, SupplyChainEnv,
                    SupplyChainMultiProduct, SupplyChainMultiProduct_IncreasingCosts, SupplyChainNPerStage,
                    SupplyChainVecEnv)
 
-__all__ = ["BeerGameEnv", "BeerGameVecEnv", "SupplyChainEnv", "SupplyChainVecEnv", "SupplyChain2perStageEnv",
+__all__ = ["BeerGameEnv", "BeerGameVecEnv", "BeerGameEnv2", "BeerGame2VecEnv", "SupplyChainEnv", "SupplyChainVecEnv", "SupplyChain2perStageEnv",
            "SupplyChainNPerStage", "SupplyChainMultiProduct", "SupplyChainMultiProduct_IncreasingCosts",
            "ENV_IDS", "VEC_ENV_IDS", "make", "make_vec", "register_gym"]
 
 # id -> entry point, as registered by the reference (gym_supplychain/__init__.py:3-51).
 # Ids whose demand model is not on the GPU path yet (seasonal / per-product demand
-# configs: beergame-v2, sc-2perstage-seasonal-v0, sc-2perstage-multiproduct-v1,
+# configs: sc-2perstage-seasonal-v0, sc-2perstage-multiproduct-v1,
 # sc-2perstage-multiproduct-inccosts-v1) are not registered.
 ENV_IDS = {
     "beergame-v0": "gym_supplychain_amd.envs:BeerGameEnv",
+    "beergame-v2": "gym_supplychain_amd.envs:BeerGameEnv2",
     "supplychain-v0": "gym_supplychain_amd.envs:SupplyChainEnv",
     "sc-2perstage-v0": "gym_supplychain_amd.envs:SupplyChain2perStageEnv",
     "sc-2perstage-multiproduct-v0": "gym_supplychain_amd.envs:SupplyChainMultiProduct",
@@ -44,6 +45,7 @@ def _sc_vec(builder):
 
 VEC_ENV_IDS = {
     "beergame-v0": BeerGameVecEnv,
+    "beergame-v2": BeerGame2VecEnv,
     "supplychain-v0": SupplyChainVecEnv,
     **{env_id: _sc_vec(b) for env_id, b in SCENARIOS.items()},
 }

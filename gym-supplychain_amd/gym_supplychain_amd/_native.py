@@ -27,10 +27,13 @@ SCG_ERR_HIP = 4
 SCG_DEMAND_FIXED = 0
 SCG_DEMAND_TABLE = 1
 SCG_DEMAND_POISSON = 2
+SCG_DEMAND_UNIFORM = 3
 
 SCG_BG_AUTORESET = 1
 SCG_STREAM_DEMAND = 0
 SCG_STREAM_ACTION = 1
+SCG_STREAM_BG2_DEMAND = 4
+SCG_STREAM_BG2_DELAY = 5
 
 BG_MAX_LEVELS = 16
 BG_MAX_WEEKS = 4096
@@ -61,7 +64,14 @@ class BgConfig(ctypes.Structure):
         ("poisson_thresholds", ctypes.c_void_p),
         ("plan", ctypes.c_void_p),
         ("ring_slots", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("variant", ctypes.c_int32),
+        ("max_stock", ctypes.c_int32),
+        ("exceeded_capacity_penalty", ctypes.c_int32),
+        ("demand_lo", ctypes.c_int32),
+        ("demand_hi", ctypes.c_int32),
+        ("stochastic_delays", ctypes.c_int32),
+        ("delay_lo", ctypes.c_int32),
+        ("delay_hi", ctypes.c_int32),
     ]
 
 
@@ -82,6 +92,7 @@ class BgState(ctypes.Structure):
         ("orders_history", ctypes.c_void_p),
         ("episode_return", ctypes.c_void_p),
         ("final_return", ctypes.c_void_p),
+        ("penalty_costs", ctypes.c_void_p),
     ]
 
 

@@ -111,7 +111,7 @@ class BeerGameVecEnv:
 
     def __init__(self, n_envs, env_init_info=None, demand="fixed", poisson_lambda=8.0, seed=0, device=None,
                  env_offset=0, auto_reset=True, track_costs=True, track_history=False, track_returns=True,
-                 horizon=None):
+                 horizon=None, config=None, variant_fields=None):
         n_envs = int(n_envs)
         if n_envs < 1:
             raise ValueError("n_envs must be >= 1")
@@ -122,17 +122,21 @@ class BeerGameVecEnv:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self._dev_index = self.device.index
         table = None
+        demand_range = (0, 0)
         if isinstance(demand, torch.Tensor):
             table = demand
             horizon = table.shape[0]
             mode = nat.SCG_DEMAND_TABLE
+        elif isinstance(demand, tuple) and len(demand) == 3 and demand[0] == "uniform":
+            mode, demand_range = nat.SCG_DEMAND_UNIFORM, (int(demand[1]), int(demand[2]))
         elif demand == "fixed":
             mode = nat.SCG_DEMAND_FIXED
         elif demand == "poisson":
             mode = nat.SCG_DEMAND_POISSON
         else:
-            raise ValueError(f"demand must be 'fixed', 'poisson' or a device tensor, got {demand!r}")
-        cfg = BeerGameConfig(env_init_info, horizon=horizon)
+            raise ValueError(f"demand must be 'fixed', 'poisson', ('uniform', lo, hi) or a device tensor, "
+                             f"got {demand!r}")
+        cfg = config if config is not None else BeerGameConfig(env_init_info, horizon=horizon)
         if mode == nat.SCG_DEMAND_FIXED and cfg.customer_demand.size < cfg.max_weeks:
             raise ValueError("customer_demand shorter than the horizon")
         self.config = cfg
@@ -156,6 +160,9 @@ class BeerGameVecEnv:
         for i, v in enumerate(cfg.initial_inventory.tolist()):
             c.initial_inventory[i] = v
         c.demand_mode = mode
+        c.demand_lo, c.demand_hi = demand_range
+        for k, v in (variant_fields or {}).items():
+            setattr(c, k, v)
         c.shipment_delays = ctypes.cast(self._delays, ctypes.c_void_p)
         c.customer_demand = ctypes.cast(self._demand, ctypes.c_void_p) if self._demand is not None else None
         c.plan = ctypes.cast(self._plan, ctypes.c_void_p)
@@ -186,6 +193,8 @@ class BeerGameVecEnv:
         self._hist = torch.zeros((T + 1, n_envs, L), **i32) if track_history else None
         self._ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
         self._final_ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
+        v2 = c.variant == 2
+        self._pen_costs = torch.zeros((n_envs, L), **i32) if (track_costs and v2) else None
         # outputs: obs and reward share one allocation so N=1 callers copy back once
         self._out = torch.zeros(n_envs * L + n_envs, **i32)
         self._obs = self._out[: n_envs * L].view(n_envs, L)
@@ -204,6 +213,7 @@ class BeerGameVecEnv:
         s.orders_history = self._hist.data_ptr() if track_history else None
         s.episode_return = self._ret.data_ptr() if track_returns else None
         s.final_return = self._final_ret.data_ptr() if track_returns else None
+        s.penalty_costs = self._pen_costs.data_ptr() if self._pen_costs is not None else None
         self._st = s
         self._cfg_ref = ctypes.byref(self._cfg)
         self._st_ref = ctypes.byref(self._st)
@@ -333,6 +343,11 @@ class BeerGameVecEnv:
         return self._bk_costs
 
     @property
+    def penalty_costs(self):
+        """BeerGameEnv2 only: [N, L] capacity-penalty ledger (beergame2_env.py:184)."""
+        return self._pen_costs
+
+    @property
     def all_orders_placed(self):
         """[N, L, T+1] like the reference's all_orders_placed (:123, :151-152)."""
         return None if self._hist is None else self._hist.permute(1, 2, 0)
@@ -450,3 +465,190 @@ class BeerGameEnv:
 
     def _observation(self):
         return self.inventory - self.backlog
+
+
+# ----------------------------------------------------------------------------------------
+# beergame-v2: BeerGameEnv2 (gym_supplychain/envs/beergame2_env.py:5-211)
+def _is_range(x):
+    """The reference reads a tuple, or a list of exactly two items, as a [low, high) range (:41, :51)."""
+    return isinstance(x, tuple) or (isinstance(x, list) and len(x) == 2)
+
+
+class _Bg2Config:
+    """BeerGameEnv2.__init__ (:10-71) resolved for the kernels."""
+
+    def __init__(self, max_stock, max_order, weeks, levels, customer_demand, initial_inventory, inv_cost, backlog_cost,
+                 exceeded_capacity_penalty, shipment_delays, initial_shipment, initial_orders):
+        self.levels = _int32("levels", levels)
+        if not 1 <= self.levels <= nat.BG_MAX_LEVELS:
+            raise ValueError(f"levels={self.levels} outside 1..{nat.BG_MAX_LEVELS}")
+        self.max_weeks = _int32("weeks", weeks)
+        if not 1 <= self.max_weeks <= nat.BG_MAX_WEEKS:
+            raise ValueError(f"weeks={self.max_weeks} outside 1..{nat.BG_MAX_WEEKS}")
+        self.max_stock = _int32("max_stock", max_stock)
+        self.max_order = _int32("max_order", max_order)
+        self.inv_cost, self.backlog_cost = _int32("inv_cost", inv_cost), _int32("backlog_cost", backlog_cost)
+        self.penalty = _int32("exceeded_capacity_penalty", exceeded_capacity_penalty)
+        self.initial_inventory = _int32_list("initial_inventory", initial_inventory)
+        if self.initial_inventory.size != self.levels:
+            raise ValueError(f"initial_inventory has {self.initial_inventory.size} entries, levels={self.levels}")
+        self.initial_shipment_value = _int32("initial_shipment", initial_shipment)
+        self.initial_orders_value = _int32("initial_orders", initial_orders)
+        T = self.max_weeks
+        self.demand_range = None
+        if _is_range(customer_demand):
+            self.demand_range = (_int32("demand low", customer_demand[0]), _int32("demand high", customer_demand[1]))
+            if self.demand_range[1] <= self.demand_range[0]:
+                raise ValueError("customer_demand range must have low < high")  # randint(low, high)
+            self.customer_demand = np.zeros(T, dtype=np.int32)
+        else:
+            self.customer_demand = _int32_list("customer_demand", customer_demand)
+            if self.customer_demand.size < T:
+                raise IndexError(f"customer_demand has {self.customer_demand.size} weeks, weeks={T}")
+        self.delay_range = None
+        if isinstance(shipment_delays, (bool, np.bool_)):
+            raise TypeError("shipment_delays must be an int, a (low, high) range or a list")
+        if isinstance(shipment_delays, (int, np.integer)):
+            self.shipment_delays = np.asarray([2] + [int(shipment_delays)] * T, dtype=np.int32)   # :50
+        elif _is_range(shipment_delays):
+            lo, hi = int(shipment_delays[0]), int(shipment_delays[1])
+            if not 0 <= lo < hi <= nat.BG_MAX_DELAY + 1:
+                raise ValueError(f"shipment delay range must satisfy 0 <= low < high <= {nat.BG_MAX_DELAY + 1}")
+            self.delay_range = (lo, hi)
+            self.shipment_delays = np.asarray([2] + [lo] * T, dtype=np.int32)
+        else:
+            self.shipment_delays = _int32_list("shipment_delays", [2] + list(shipment_delays))         # :55
+            if self.shipment_delays.size < T + 1:
+                raise IndexError(f"shipment_delays needs {T} entries")
+            self.shipment_delays = self.shipment_delays[: T + 1].copy()
+        if self.shipment_delays.min() < 0 or self.shipment_delays.max() > nat.BG_MAX_DELAY:
+            raise ValueError(f"shipment delays must be within 0..{nat.BG_MAX_DELAY}")
+
+
+class BeerGame2VecEnv(BeerGameVecEnv):
+    """N lock-step BeerGameEnv2 envs: same keywords as the reference class (:10-14).
+
+    Observations are int32 `max_stock + inventory - backlog`; actions are the absolute
+    orders (int32 [N, L]); rewards include the capacity penalty. A (low, high)
+    customer_demand or shipment_delays draws randint(low, high) per (env, episode, week)
+    on device with Philox (streams 4 and 5) where the reference uses RandomState (:76-92).
+    """
+
+    def __init__(self, n_envs, max_stock=100, max_order=30, weeks=35, levels=4, customer_demand=None,
+                 initial_inventory=(12, 12, 12, 12), inv_cost=1, backlog_cost=2, exceeded_capacity_penalty=100,
+                 shipment_delays=2, initial_shipment=4, initial_orders=4, seed=None, device=None, env_offset=0,
+                 auto_reset=True, track_costs=True, track_history=False, track_returns=True):
+        if customer_demand is None:
+            customer_demand = [4] * 4 + [8] * 31
+        cfg = _Bg2Config(max_stock, max_order, weeks, levels, customer_demand, list(initial_inventory), inv_cost,
+                         backlog_cost, exceeded_capacity_penalty, shipment_delays, initial_shipment, initial_orders)
+        fields = dict(variant=2, max_stock=cfg.max_stock, exceeded_capacity_penalty=cfg.penalty)
+        if cfg.delay_range:
+            fields.update(stochastic_delays=1, delay_lo=cfg.delay_range[0], delay_hi=cfg.delay_range[1])
+        demand = ("uniform",) + cfg.demand_range if cfg.demand_range else "fixed"
+        super().__init__(n_envs, None, demand=demand, seed=0 if seed is None else seed, device=device,
+                         env_offset=env_offset, auto_reset=auto_reset, track_costs=track_costs,
+                         track_history=track_history, track_returns=track_returns, config=cfg, variant_fields=fields)
+        self.max_stock, self.max_order = cfg.max_stock, cfg.max_order
+        L = cfg.levels
+        self.single_observation_space = spaces.Box(0, 2 * cfg.max_stock - 1, (L,), np.int32)   # MultiDiscrete (:28)
+        self.single_action_space = spaces.Box(0, cfg.max_order - 1, (L,), np.int32)            # MultiDiscrete (:27)
+
+    def rollout(self, *a, **k):
+        raise NotImplementedError("rollout is not implemented for BeerGameEnv2")
+
+
+class BeerGameEnv2:
+    """Drop-in for gym_supplychain.envs.BeerGameEnv2 (beergame2_env.py:5-211), one env.
+
+    reset() -> int64 observation; step(action) -> (int64 obs, Python int reward, bool, {});
+    inventory_costs / backlog_costs / penalty_costs are float64 like the reference's.
+    """
+
+    def __init__(self, max_stock=100, max_order=30, weeks=35, levels=4, customer_demand=[4] * 4 + [8] * 31,  # noqa: B006
+                 initial_inventory=[12, 12, 12, 12], inv_cost=1, backlog_cost=2,  # noqa: B006
+                 exceeded_capacity_penalty=100, shipment_delays=2, initial_shipment=4, initial_orders=4, seed=None,
+                 device=None):
+        self.DEBUG = False
+        self._vec = BeerGame2VecEnv(1, max_stock, max_order, weeks, levels, customer_demand, initial_inventory,
+                                    inv_cost, backlog_cost, exceeded_capacity_penalty, shipment_delays,
+                                    initial_shipment, initial_orders, seed=seed, device=device, auto_reset=False,
+                                    track_costs=True, track_history=True, track_returns=False)
+        self.levels, self.max_stock, self.max_weeks = levels, max_stock, weeks
+        self.action_space = spaces.Box(0, max_order - 1, (levels,), np.int64)
+        self.observation_space = spaces.Box(0, 2 * max_stock - 1, (levels,), np.int64)
+        self.current_state = None
+        self.week = None
+        pin = torch.cuda.is_available()
+        self._act_host = torch.zeros((1, levels), dtype=torch.int32, pin_memory=pin)
+        self._act_np = self._act_host.numpy()
+        self._act_dev = torch.zeros((1, levels), dtype=torch.int32, device=self._vec.device)
+        self._out_host = torch.zeros(self._vec._out.shape, dtype=torch.int32, pin_memory=pin)
+        self._out_np = self._out_host.numpy()
+
+    def seed(self, seed=None):
+        self._vec._st.seed = 0 if seed is None else int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._vec._st.episode, self._vec._st.week = 0, -1
+
+    def reset(self):
+        obs = self._vec.reset()
+        self.week = 0
+        self.current_state = obs[0].cpu().numpy().astype(np.int64)
+        return self.current_state
+
+    def step(self, action):
+        if self.week is None:
+            raise AttributeError("'BeerGameEnv2' object has no attribute 'week' (call reset() first)")
+        self._act_np[0, :] = np.asarray(action).astype(np.int64).reshape(-1)
+        self._act_dev.copy_(self._act_host, non_blocking=True)
+        self._vec.step(self._act_dev)
+        self._out_host.copy_(self._vec._out, non_blocking=True)
+        torch.cuda.current_stream(self._vec.device).synchronize()
+        L = self.levels
+        self.week = self._vec.week
+        self.current_state = self._out_np[:L].astype(np.int64)
+        return self.current_state, int(self._out_np[L]), self.week == self.max_weeks, {}
+
+    def _row(self, t, dtype=np.int64):
+        return t[0].cpu().numpy().astype(dtype)
+
+    @property
+    def inventory(self):
+        return self._row(self._vec.inventory)
+
+    @property
+    def backlog(self):
+        return self._row(self._vec.backlog)
+
+    @property
+    def orders_placed(self):
+        return self._row(self._vec.orders_placed)
+
+    @property
+    def inventory_costs(self):
+        return self._row(self._vec.inventory_costs, np.float64)
+
+    @property
+    def backlog_costs(self):
+        return self._row(self._vec.backlog_costs, np.float64)
+
+    @property
+    def penalty_costs(self):
+        return self._row(self._vec.penalty_costs, np.float64)
+
+    @property
+    def all_orders_placed(self):
+        return self._vec.all_orders_placed[0].cpu().numpy().astype(np.int64)
+
+    def render(self, mode='human'):
+        inv, bk = self.inventory, self.backlog
+        print('\n' + '=' * 20)
+        print('Week:\t', self.week)
+        print('Inventory/back:\t', inv, bk, inv - bk)
+        print('Orders placed:\t', self.orders_placed)
+        print('Inventory costs:', self.inventory_costs)
+        print('Backlog costs:\t', self.backlog_costs)
+        print('Penalty costs:\t', self.penalty_costs)
+
+    def close(self):
+        pass

@@ -61,7 +61,8 @@ typedef enum scg_status {
 typedef enum scg_demand_mode {
   SCG_DEMAND_FIXED = 0,   /* one list shared by all envs: customer_demand (beergame_env.py:33) */
   SCG_DEMAND_TABLE = 1,   /* per-env device table int32 [T][N] (caller-drawn demand)            */
-  SCG_DEMAND_POISSON = 2  /* per-(env, episode, week) Poisson draw on device, Philox4x32-10     */
+  SCG_DEMAND_POISSON = 2, /* per-(env, episode, week) Poisson draw on device, Philox4x32-10     */
+  SCG_DEMAND_UNIFORM = 3  /* per-(env, episode, week) randint(demand_lo, demand_hi), Philox     */
 } scg_demand_mode;
 
 /* Step flags */
@@ -70,6 +71,8 @@ typedef enum scg_demand_mode {
 /* Philox streams (counter word 3) */
 #define SCG_STREAM_DEMAND 0u
 #define SCG_STREAM_ACTION 1u
+#define SCG_STREAM_BG2_DEMAND 4u
+#define SCG_STREAM_BG2_DELAY 5u
 
 /*
  * Env configuration, the resolved form of BeerGameEnv's env_init_info
@@ -91,7 +94,13 @@ typedef struct scg_bg_config {
   const uint32_t* poisson_thresholds; /* DEVICE [poisson_len] (scg_poisson_table)       */
   int32_t* plan;                  /* HOST [T+1] workspace, filled by scg_bg_prepare     */
   int32_t ring_slots;             /* out of scg_bg_prepare: R = max delay + 1           */
-  int32_t reserved;
+  /* BeerGameEnv2 (beergame2_env.py:5-211) when variant == 2 ----------------------------- */
+  int32_t variant;                /* 1: BeerGameEnv, 2: BeerGameEnv2                    */
+  int32_t max_stock;              /* v2: observation offset and capacity (:24, :112)    */
+  int32_t exceeded_capacity_penalty; /* v2: per unit beyond max_stock (:35, :179-180)  */
+  int32_t demand_lo, demand_hi;   /* SCG_DEMAND_UNIFORM: randint(lo, hi) per week (:77) */
+  int32_t stochastic_delays;      /* v2: per-episode randint(delay_lo, delay_hi) (:91)  */
+  int32_t delay_lo, delay_hi;
 } scg_bg_config;
 
 /*
@@ -113,6 +122,7 @@ typedef struct scg_bg_state {
   int32_t* orders_history;  /* [T+1][N][L] self.all_orders_placed :123 (optional)       */
   int64_t* episode_return;  /* [N] running sum of rewards (optional)                   */
   int64_t* final_return;    /* [N] episode_return at the terminal week (optional)      */
+  int32_t* penalty_costs;   /* [N][L]  v2 self.penalty_costs :184 (optional)           */
 } scg_bg_state;
 
 /* ABI version (SCG_ABI_VERSION of the built library). */

@@ -40,3 +40,15 @@ def load_sc(name):
     g["meta"] = json.loads(str(g["meta"]))
     g["oracle_kwargs"] = {k: g["meta"]["kwargs"][k] for k in SC_ORACLE_KW if k in g["meta"]["kwargs"]}
     return g
+
+
+# ---- BeerGameEnv2 (written by oracle/gen_golden_bg2.py) --------------------------------
+def beergame2_cases():
+    return sorted(os.path.basename(p)[len("beergame2_"):-4] for p in glob.glob(os.path.join(GOLDEN, "beergame2_*.npz")))
+
+
+def load_beergame2(name):
+    import ast
+    g = dict(np.load(os.path.join(GOLDEN, f"beergame2_{name}.npz")))
+    g["kwargs"] = ast.literal_eval(str(g["kwargs"]))
+    return g

@@ -253,3 +253,60 @@ def test_timed_step_matches_and_stamps_kernel():
     for s, e in evs:
         nat.hip_event_destroy(s)
         nat.hip_event_destroy(e)
+
+
+# ---- BeerGameEnv2 ----------------------------------------------------------------------
+from golden_io import beergame2_cases, load_beergame2  # noqa: E402
+
+
+@pytest.mark.parametrize("name", beergame2_cases())
+def test_beergame2_matches_reference(name):
+    from gym_supplychain_amd import BeerGame2VecEnv
+    g = load_beergame2(name)
+    T, N, L = g["actions"].shape
+    kw = dict(g["kwargs"])
+    for k in ("customer_demand", "shipment_delays"):
+        if isinstance(kw.get(k), list) and len(kw[k]) == 2:
+            kw[k] = tuple(kw[k])
+    env = BeerGame2VecEnv(N, seed=int(g["seed"]), device=DEV, auto_reset=False, track_history=True, **kw)
+    for _ in range(int(g["episode"])):
+        env.reset()
+    obs = env.reset()
+    assert np.array_equal(obs.cpu().numpy(), g["ref_reset_obs"])
+    acts = _i32(g["actions"])
+    for w in range(T):
+        obs, rew, done, _ = env.step(acts[w])
+        assert np.array_equal(obs.cpu().numpy(), g["ref_obs"][w]), (name, w)
+        assert np.array_equal(rew.cpu().numpy(), g["ref_reward"][w]), (name, w)
+        assert np.array_equal(env.inventory.cpu().numpy(), g["ref_inventory"][w])
+        assert np.array_equal(env.backlog.cpu().numpy(), g["ref_backlog"][w])
+        assert np.array_equal(env.orders_placed.cpu().numpy(), g["ref_orders_placed"][w])
+    for k in ("inventory_costs", "backlog_costs", "penalty_costs"):
+        assert np.array_equal(getattr(env, k).cpu().numpy().astype(np.float64), g["ref_" + k])
+    with pytest.raises(IndexError):
+        env.step(acts[0])
+
+
+def test_beergame2_facade_and_autoreset():
+    from gym_supplychain_amd import BeerGame2VecEnv, BeerGameEnv2
+    g = load_beergame2("defaults")
+    T, N, L = g["actions"].shape
+    e = BeerGameEnv2()
+    o = e.reset()
+    assert o.dtype == np.int64 and np.array_equal(o, g["ref_reset_obs"][0])
+    for w in range(T):
+        obs, r, done, info = e.step(g["actions"][w, 0])
+        assert np.array_equal(obs, g["ref_obs"][w, 0]) and r == g["ref_reward"][w, 0] and type(r) is int
+        assert done == (w == T - 1) and info == {}
+    assert e.penalty_costs.dtype == np.float64 and np.array_equal(e.penalty_costs, g["ref_penalty_costs"][0])
+    # auto-reset with stochastic draws: the second episode draws fresh tables
+    v = BeerGame2VecEnv(256, customer_demand=(0, 16), shipment_delays=(0, 5), seed=3, device=DEV)
+    v.reset()
+    a = torch.full((256, 4), 5, dtype=torch.int32, device=DEV)
+    rets = []
+    for ep in range(2):
+        for w in range(35):
+            _, _, done, info = v.step(a)
+        assert bool(done.all())
+        rets.append(info["episode_return"].clone())
+    assert not torch.equal(rets[0], rets[1])

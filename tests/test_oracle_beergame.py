@@ -71,3 +71,35 @@ def test_poisson_table_edges():
         poisson_thresholds(-1.0)
     with pytest.raises(ValueError):
         poisson_thresholds(1000.0)
+
+
+# ---- BeerGameEnv2 ----------------------------------------------------------------------
+from golden_io import beergame2_cases, load_beergame2  # noqa: E402
+from oracle.beergame import BeerGame2Oracle  # noqa: E402
+
+
+@pytest.mark.parametrize("name", beergame2_cases())
+def test_beergame2_oracle_matches_reference(name):
+    g = load_beergame2(name)
+    T, N, L = g["actions"].shape
+    kw = {k: v for k, v in g["kwargs"].items() if k not in ("customer_demand", "shipment_delays", "max_order",
+                                                              "weeks", "levels")}
+    for n in range(N):
+        o = BeerGame2Oracle(weeks=T, levels=L, customer_demand=g["demand"][n], shipment_delays=g["delays"][n].tolist(),
+                            **kw)
+        assert np.array_equal(o.reset(), g["ref_reset_obs"][n])
+        for w in range(T):
+            obs, r, done, info = o.step(g["actions"][w, n])
+            assert np.array_equal(obs, g["ref_obs"][w, n]) and r == g["ref_reward"][w, n] and isinstance(r, int)
+        for k in ("inventory_costs", "backlog_costs", "penalty_costs"):
+            assert np.array_equal(getattr(o, k), g["ref_" + k][n])
+
+
+def test_beergame2_tables_are_philox_draws():
+    import sys
+    sys.path.insert(0, "oracle")
+    from oracle.gen_golden_bg2 import CASES, case_tables
+    for name in beergame2_cases():
+        g = load_beergame2(name)
+        demand, delays = case_tables(CASES[name])
+        assert np.array_equal(demand, g["demand"]) and np.array_equal(delays, g["delays"])
