@@ -12,10 +12,11 @@ from . import _native  # noqa: F401  (fails loudly when libscgpu.so is missing)
 from .envs import (SCENARIOS, BeerGame2VecEnv, BeerGameEnv, BeerGameEnv2, BeerGameVecEnv, SupplyChain2perStageEnv, SupplyChainEnv,
                    SupplyChainMultiProduct, SupplyChainMultiProduct_IncreasingCosts, SupplyChainNPerStage,
                    SupplyChainVecEnv)
+from .vec_env import SB3VecEnv
 
 __all__ = ["BeerGameEnv", "BeerGameVecEnv", "BeerGameEnv2", "BeerGame2VecEnv", "SupplyChainEnv", "SupplyChainVecEnv", "SupplyChain2perStageEnv",
            "SupplyChainNPerStage", "SupplyChainMultiProduct", "SupplyChainMultiProduct_IncreasingCosts",
-           "ENV_IDS", "VEC_ENV_IDS", "make", "make_vec", "register_gym"]
+           "SB3VecEnv", "ENV_IDS", "VEC_ENV_IDS", "make", "make_vec", "register_gym"]
 
 # id -> entry point, as registered by the reference (gym_supplychain/__init__.py:3-51).
 # Ids whose demand model is not on the GPU path yet (seasonal / per-product demand

@@ -239,6 +239,11 @@ class BeerGameVecEnv:
         nat.check(nat.lib.scg_bg_reset(self._cfg_ref, self._st_ref, self._obs.data_ptr(), self._stream()))
         return self._obs
 
+    def seed(self, seed=None):
+        """New Philox key; the next reset() starts episode 0 again."""
+        self._st.seed = 0 if seed is None else int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._st.episode, self._st.week = 0, -1
+
     def _actions(self, actions):
         N, L = self.n_envs, self.levels
         if not isinstance(actions, torch.Tensor):
@@ -587,8 +592,7 @@ class BeerGameEnv2:
         self._out_np = self._out_host.numpy()
 
     def seed(self, seed=None):
-        self._vec._st.seed = 0 if seed is None else int(seed) & 0xFFFFFFFFFFFFFFFF
-        self._vec._st.episode, self._vec._st.week = 0, -1
+        self._vec.seed(seed)
 
     def reset(self):
         obs = self._vec.reset()
