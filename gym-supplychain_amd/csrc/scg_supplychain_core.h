@@ -127,14 +127,49 @@ __host__ __device__ inline void sc_reset_env(const ScCtx& c, ScEnv& e) {
   }
 }
 
+// MAXD scalars with their NumPy kinds, the kinds packed 4 bits per entry so an unrolled
+// array costs 2 VGPRs per entry plus one word per 8 entries (not 3 per entry as Num[]).
+template <int MAXD>
+struct NumVec {
+  double v[MAXD];
+  uint32_t kw[(MAXD + 7) / 8];
+  __host__ __device__ __forceinline__ Num get(int i) const {
+    return Num{v[i], static_cast<int>((kw[i >> 3] >> (4 * (i & 7))) & 15u)};
+  }
+  __host__ __device__ __forceinline__ void set(int i, Num x) {
+    v[i] = x.v;
+    const uint32_t sh = 4u * static_cast<uint32_t>(i & 7);
+    kw[i >> 3] = (kw[i >> 3] & ~(15u << sh)) | (static_cast<uint32_t>(x.k) << sh);
+  }
+  // Runtime index without dynamic register indexing (which would put the array in
+  // scratch): an unrolled select; constant-folds to get()/set() when i is known.
+  __host__ __device__ __forceinline__ Num get_dyn(int i) const {
+    double x = 0.0;
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j) x = (j == i) ? v[j] : x;
+#pragma unroll
+    for (int j = 0; j < (MAXD + 7) / 8; ++j) w = (j == (i >> 3)) ? kw[j] : w;
+    return Num{x, static_cast<int>((w >> (4 * (i & 7))) & 15u)};
+  }
+  __host__ __device__ __forceinline__ void set_dyn(int i, Num x) {
+    const uint32_t sh = 4u * static_cast<uint32_t>(i & 7);
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j) v[j] = (j == i) ? x.v : v[j];
+#pragma unroll
+    for (int j = 0; j < (MAXD + 7) / 8; ++j)
+      kw[j] = (j == (i >> 3)) ? ((kw[j] & ~(15u << sh)) | (static_cast<uint32_t>(x.k) << sh)) : kw[j];
+  }
+};
+
 // SC_Action.apply for SHIP (:58-96): the cut [0, limit] split at the destinations'
 // sorted action values; amount_i = (v_(k) - v_(k-1)) * limit, clamped to what is left.
 // Sorting (value, index) tuples is done by ranks so every array index is a compile-time
 // constant (MAXD-unrolled loops): the arrays stay in registers instead of scratch.
 template <int MAXD>
-__host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num limit, Num (&out)[MAXD]) {
+__host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num limit, NumVec<MAXD>& out) {
 #pragma unroll
-  for (int i = 0; i < MAXD; ++i) out[i] = pyint(0);
+  for (int i = 0; i < MAXD; ++i) out.set(i, pyint(0));
   Num left = limit;
   if (!np_lt(pyint(0), left)) return;
   int rank[MAXD];
@@ -160,7 +195,7 @@ __host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num l
     if (np_lt(left, amt)) amt = left;
 #pragma unroll
     for (int i = 0; i < MAXD; ++i)
-      if (i < D && rank[i] == s) out[i] = amt;
+      if (i < D && rank[i] == s) out.set(i, amt);
     left = np_sub(left, amt);
     prev = v;
     first = false;
@@ -216,64 +251,58 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
   if (!nd.last_level) {
     // SHIP (:262-375)
     const int D = nd.n_dests;
-    Num ship_left[MAXD];
+    NumVec<MAXD> ship_left;  // available_ship_capacities, shared by the products (:265)
 #pragma unroll
-    for (int i = 0; i < MAXD; ++i) ship_left[i] = pyint(i < D ? nd.ship_capacity[i] : 0);
+    for (int i = 0; i < MAXD; ++i) ship_left.set(i, pyint(i < D ? nd.ship_capacity[i] : 0));
     Num proc_left = pyint(nd.processing_capacity);
     const int lt_base = lt_i;
+    const bool factory = nd.processing_capacity > 0;
     for (int p = 0; p < P; ++p) {
       if (!(nd.stock_capacity[p] > 0)) continue;  // no SHIP action for this product
       Num over_ship = pyint(0), over_proc = pyint(0);
       const Num material = f64(sc_stock(c, e, ni, p));
       if (np_lt(pyint(0), material)) {
         float vals[MAXD];
-        Num out[MAXD], sent[MAXD];
+        NumVec<MAXD> out;
 #pragma unroll
         for (int i = 0; i < MAXD; ++i) vals[i] = i < D ? static_cast<float>(sc_action(act, nd.action_offset + a_i + i).v) : 0.0f;
         sc_split<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), out);
-#pragma unroll
-        for (int i = 0; i < MAXD; ++i) sent[i] = out[i];
-        if (nd.processing_capacity > 0) {  // factory: processing capacity and ratio (:298-310)
-#pragma unroll
-          for (int i = 0; i < MAXD; ++i) {
-            if (i < D) {
-              if (np_lt(pyint(0), out[i])) {
-                if (np_lt(proc_left, out[i])) {
-                  over_proc = np_add(over_proc, np_sub(out[i], proc_left));
-                  out[i] = proc_left;
-                }
-                proc_left = np_sub(proc_left, out[i]);
+        // The reference's per-destination passes — processing capacity and ratio
+        // (:298-310), ship capacity (:312-328), sum(amounts) (:331), the pushes (:344-348)
+        // and sum(calculate_costs(amounts_to_ship)) (:352) — each carry their own
+        // accumulator in destination order and read only destination i's values; the
+        // stock update between them (:332) touches none of them. So they run fused, one
+        // destination at a time, every accumulator seeing the reference's order, and no
+        // per-destination array besides the split's output stays live.
+        Num leaving = pyint(0), ship_cost = pyint(0);
+        for (int i = 0; i < D; ++i) {  // rolled: the body holds a heap push
+          Num o = out.get_dyn(i);
+          Num snt = o;  // amounts_to_ship = amounts.copy() (:292)
+          if (factory) {
+            if (np_lt(pyint(0), o)) {
+              if (np_lt(proc_left, o)) {
+                over_proc = np_add(over_proc, np_sub(o, proc_left));
+                o = proc_left;
               }
-              sent[i] = np_div(out[i], pyint(nd.processing_ratio[p]));
+              proc_left = np_sub(proc_left, o);
             }
+            snt = np_div(o, pyint(nd.processing_ratio[p]));
           }
-        }
-#pragma unroll
-        for (int i = 0; i < MAXD; ++i) {  // per-destination ship capacity (:312-328)
-          const Num amt = sent[i];
-          if (i < D && np_lt(pyint(0), amt) && np_lt(ship_left[i], amt)) {
-            over_ship = np_add(over_ship, np_sub(amt, ship_left[i]));
-            sent[i] = ship_left[i];
-            out[i] = nd.processing_capacity > 0 ? np_mul(sent[i], pyint(nd.processing_ratio[p])) : sent[i];
-            ship_left[i] = np_sub(ship_left[i], out[i]);  // only on overflow, by out[i]
+          const Num cap = ship_left.get_dyn(i);
+          if (np_lt(pyint(0), snt) && np_lt(cap, snt)) {
+            over_ship = np_add(over_ship, np_sub(snt, cap));
+            snt = cap;
+            o = factory ? np_mul(snt, pyint(nd.processing_ratio[p])) : snt;
+            ship_left.set_dyn(i, np_sub(cap, o));  // only on overflow, by the new amount
           }
+          leaving = np_add(leaving, o);
+          if (np_lt(pyint(0), snt))
+            sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
+          ship_cost = np_add(ship_cost, np_mul(snt, pyint(nd.dest_costs[p][i])));
         }
-        Num leaving = pyint(0);  // sum(amounts) (:331)
-#pragma unroll
-        for (int i = 0; i < MAXD; ++i)
-          if (i < D) leaving = np_add(leaving, out[i]);
         double& st = sc_stock(c, e, ni, p);
         st = st - leaving.v;  // float64 array element minus the promoted scalar (:332)
-        if (nd.processing_capacity > 0) cost = np_add(cost, np_mul(leaving, pyint(nd.processing_cost[p])));
-        Num ship_cost = pyint(0);  // sum(calculate_costs(amounts_to_ship)) (:352)
-#pragma unroll
-        for (int i = 0; i < MAXD; ++i) {  // (:344-348)
-          if (i < D) {
-            if (np_lt(pyint(0), sent[i]))
-              sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), sent[i]);
-            ship_cost = np_add(ship_cost, np_mul(sent[i], pyint(nd.dest_costs[p][i])));
-          }
-        }
+        if (factory) cost = np_add(cost, np_mul(leaving, pyint(nd.processing_cost[p])));
         cost = np_add(cost, ship_cost);
       }
       cost = np_add(cost, np_mul(pyint(c.pen_proc), over_proc));  // :361

@@ -9,7 +9,10 @@ so these are submission costs while the GPU drains behind them):
   torch_tiny_launch  a tiny torch elementwise op (HIP launch floor as torch pays it)
   step_loop          the bench loop: env.step(week[env.week]) (kernel launched)
   step_loop_wall_us  same, wall time per step including the drain at the end
-and the kernel time per step from kernel-stamped events for comparison.
+and the kernel time per step from kernel-stamped events for comparison, plus torch's device
+copy of the step kernel's byte count (17.05 MB: half read, half written) and of 4x that,
+as the practical bandwidth ceiling at this working-set size (back-to-back launches, so the
+figure includes launch gaps; an upper bound on per-launch time).
 """
 import argparse
 import json
@@ -77,6 +80,22 @@ def main():
     for s, e in ev:
         nat.hip_event_destroy(s)
         nat.hip_event_destroy(e)
+    # practical ceiling at this size: torch's own copy of the same byte count (half read,
+    # half written) and a 4x larger one, timed with events on the current stream
+    for tag, nbytes in (("copy_same_bytes", 17054339), ("copy_4x_bytes", 4 * 17054339)):
+        n = nbytes // 8
+        src = torch.ones(n, dtype=torch.int32, device=dev)
+        dst = torch.empty_like(src)
+        for _ in range(20):
+            dst.copy_(src)
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        for _ in range(200):
+            dst.copy_(src)
+        s1.record()
+        torch.cuda.synchronize()
+        us = s0.elapsed_time(s1) / 200 * 1e3
+        out[tag] = {"bytes": 2 * n * 4, "us": us, "GBps": 2 * n * 4 / us / 1e3}
     out["n_envs"] = N
     print(json.dumps(out), flush=True)
 
