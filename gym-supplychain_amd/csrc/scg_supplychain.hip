@@ -15,6 +15,7 @@
 
 #include "scg_common.h"
 #include "scg_supplychain_core.h"
+#include "scg_supplychain_level.h"
 #include "scgpu.h"
 
 namespace scg {
@@ -40,6 +41,7 @@ struct ScArgs {
   int32_t t;       // the step being simulated (1..T) / 0 for reset
   int32_t flags;   // bit0 terminal, bit1 autoreset
   int32_t obs_f64;
+  int32_t layout;  // SCG_SC_LAYOUT_*
 };
 
 struct ObsRow {
@@ -55,6 +57,11 @@ struct ObsRow {
 };
 
 __device__ __forceinline__ ScEnv env_view(const ScArgs& a, int64_t n, uint32_t episode) {
+  if (a.layout == SCG_SC_LAYOUT_ENV_MAJOR) {  // env n's block: [NP], [NP][H]
+    const int64_t NP = static_cast<int64_t>(a.c.n_nodes) * a.c.P;
+    return ScEnv{a.stock + n * NP, a.tk + n * NP * a.c.H, a.val + n * NP * a.c.H, a.size + n * NP, 1, 1,
+                 static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
+  }
   return ScEnv{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, a.n, static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
 }
 
@@ -172,6 +179,64 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
   }
 }
 
+// Level-parallel step (scg_supplychain_level.h): G lanes per env, 64 / G envs per block,
+// env-major state so one env's heaps are a contiguous block that stays cache-resident
+// while its group works on it; the level inbox and node costs live in LDS.
+struct DevSched {
+  int G, s;
+  bool live;
+  template <class F>
+  __device__ __forceinline__ void phase(F&& f) {
+    if (live) f(s);
+    __syncthreads();
+  }
+};
+
+__device__ __forceinline__ size_t level_env_lds(const ScCtx& c, int inbox) {
+  return ((static_cast<size_t>(c.n_nodes) * sizeof(Num) + static_cast<size_t>(inbox) * 12 + 15) / 16) * 16;
+}
+
+template <int MAXD>
+__global__ __launch_bounds__(kScBlock) void sc_level_kernel(const ScArgs a, const ScLevels lv, int G, int inbox) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const ScCtx& c = a.c;
+  const int g = threadIdx.x / G;
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * (kScBlock / G) + g;
+  DevSched sch{G, static_cast<int>(threadIdx.x) % G, n < a.n};
+  unsigned char* mine = smem + g * level_env_lds(c, inbox);
+  ScLevelEnv x;
+  x.cost = reinterpret_cast<Num*>(mine);
+  x.in_val = reinterpret_cast<double*>(mine + c.n_nodes * sizeof(Num));
+  x.in_tk = reinterpret_cast<int32_t*>(x.in_val + inbox);
+  const int64_t m = sch.live ? n : 0;  // idle groups (tail block) only join the barriers
+  x.e = env_view(a, m, a.episode);
+  x.act = a.act + m * c.A;
+  const double reward = sc_level_step<MAXD>(c, lv, x, a.t, sch);
+  const bool terminal = a.flags & 1;
+  if (sch.live && sch.s == 0) {
+    a.rew[n] = reward;
+    if (a.ep_ret) {
+      const double r = a.ep_ret[n] + reward;
+      if (terminal && a.final_ret) a.final_ret[n] = r;
+      a.ep_ret[n] = (a.flags & 2) ? 0.0 : r;
+    }
+  }
+  ObsRow out{a.obs, m * c.O, a.obs_f64};
+  ObsRow tout{a.term_obs, m * c.O, a.obs_f64};
+  if (a.flags & 2) {
+    if (a.term_obs) sch.phase([&](int s) { sc_level_observe_lane(c, x.e, a.t, tout, s, G); });
+    x.e.episode = a.episode + 1;
+    sch.phase([&](int s) { sc_level_reset_lane(c, x.e, s, G); });
+    sch.phase([&](int s) { sc_level_observe_lane(c, x.e, 0, out, s, G); });
+  } else {
+    sch.phase([&](int s) {
+      sc_level_observe_lane(c, x.e, a.t, out, s, G);
+      if (terminal && a.term_obs) sc_level_observe_lane(c, x.e, a.t, tout, s, G);
+    });
+  }
+  if (sch.live && x.e.overflow) atomicOr(a.err, 1);
+}
+
 __global__ __launch_bounds__(kScBlock) void sc_tables_kernel(const ScArgs a, int32_t* __restrict__ demand,
                                                              int32_t* __restrict__ leadtimes) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
@@ -246,6 +311,7 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   a.env_offset = st->env_offset;
   a.episode = st->episode;
   a.obs_f64 = cfg->obs_f64;
+  a.layout = cfg->layout;
   return a;
 }
 
@@ -253,6 +319,52 @@ dim3 sc_grid(int64_t n) { return dim3(static_cast<unsigned>((n + kScBlock - 1) /
 
 // LDS the staged step kernel needs per 64-env block; staged only while >= 2 blocks fit a CU.
 constexpr size_t kScLdsMax = 64 * 1024;
+
+// LDS of the level kernel per block: (64 / G) envs x (node costs + inbox), as level_env_lds.
+size_t sc_level_lds_bytes(const scg_sc_config* cfg) {
+  const size_t per_env = ((static_cast<size_t>(cfg->n_nodes) * sizeof(Num) + static_cast<size_t>(cfg->inbox_size) * 12 + 15) / 16) * 16;
+  return static_cast<size_t>(kScBlock / cfg->group) * per_env;
+}
+
+// The level schedule of a chain (scg_supplychain_level.h), or false when it has none:
+// every shipment must go from a node to a later node exactly one level down, levels must be
+// runs of consecutive nodes, and no node may list a destination twice.
+bool sc_level_schedule(scg_sc_config* cfg, const scg_sc_node* nodes) {
+  const int NN = cfg->n_nodes;
+  std::vector<int> lvl(NN, 0);
+  for (int i = 0; i < NN; ++i)
+    for (int d = 0; d < nodes[i].n_dests; ++d) {
+      const int j = nodes[i].dests[d];
+      if (j <= i) return false;
+      for (int d2 = 0; d2 < d; ++d2)
+        if (nodes[i].dests[d2] == j) return false;
+      lvl[j] = std::max(lvl[j], lvl[i] + 1);
+    }
+  for (int i = 0; i < NN; ++i) {
+    if (i > 0 && lvl[i] != lvl[i - 1] && lvl[i] != lvl[i - 1] + 1) return false;
+    for (int d = 0; d < nodes[i].n_dests; ++d)
+      if (lvl[nodes[i].dests[d]] != lvl[i] + 1) return false;
+  }
+  if (lvl[0] != 0 || lvl[NN - 1] + 1 > SCG_SC_MAX_LEVELS) return false;
+  const int L = lvl[NN - 1] + 1;
+  int wmax = 1, inbox = 1;
+  for (int l = 0, i = 0; l < L; ++l) {
+    cfg->level_start[l] = i;
+    while (i < NN && lvl[i] == l) ++i;
+  }
+  cfg->level_start[L] = NN;
+  for (int l = 0; l < L; ++l) {
+    const int w = cfg->level_start[l + 1] - cfg->level_start[l];
+    wmax = std::max(wmax, w);
+    if (l + 1 < L) inbox = std::max(inbox, cfg->n_products * w * (cfg->level_start[l + 2] - cfg->level_start[l + 1]));
+  }
+  int G = 1;
+  while (G < wmax && G < kScBlock) G *= 2;
+  cfg->n_levels = L;
+  cfg->group = G;
+  cfg->inbox_size = inbox;
+  return sc_level_lds_bytes(cfg) <= kScLdsMax;
+}
 size_t sc_lds_bytes(const scg_sc_config* cfg) {
   const size_t NP = static_cast<size_t>(cfg->n_nodes) * cfg->n_products;
   return kScBlock * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
@@ -347,6 +459,18 @@ int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
   cfg->n_obs = n_ret * P + NN * P + NN * P * cfg->avg_leadtime + 1;
   cfg->heap_capacity = H;
   cfg->max_dests = maxd;
+  // kernel: the level-parallel one whenever the chain has a level schedule
+  const int want = cfg->kernel;
+  if (want != SCG_SC_KERNEL_AUTO && want != SCG_SC_KERNEL_LANE && want != SCG_SC_KERNEL_LEVEL)
+    return fail(SCG_ERR_INVALID, "kernel=%d is not a SCG_SC_KERNEL_* value", want);
+  cfg->n_levels = 0;
+  cfg->group = 1;
+  cfg->inbox_size = 0;
+  const bool levels = want != SCG_SC_KERNEL_LANE && sc_level_schedule(cfg, nodes);
+  if (want == SCG_SC_KERNEL_LEVEL && !levels)
+    return fail(SCG_ERR_INVALID, "the chain has no level schedule (shipments must go to the next run of nodes)");
+  cfg->kernel = levels ? SCG_SC_KERNEL_LEVEL : SCG_SC_KERNEL_LANE;
+  cfg->layout = levels ? SCG_SC_LAYOUT_ENV_MAJOR : SCG_SC_LAYOUT_ENV_FASTEST;
   return SCG_OK;
 }
 
@@ -381,7 +505,26 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
   const dim3 grid = sc_grid(st->n_envs);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t lds = sc_lds_bytes(cfg);
-  if (lds <= kScLdsMax) {
+  if (cfg->kernel == SCG_SC_KERNEL_LEVEL) {
+    if (cfg->layout != SCG_SC_LAYOUT_ENV_MAJOR || cfg->n_levels < 1 || cfg->group < 1 || cfg->group > kScBlock)
+      return fail(SCG_ERR_INVALID, "level kernel needs the schedule scg_sc_prepare derives");
+    ScLevels lv;
+    lv.n = cfg->n_levels;
+    for (int l = 0; l <= SCG_SC_MAX_LEVELS; ++l) lv.start[l] = cfg->level_start[l];
+    const int per_block = kScBlock / cfg->group;
+    const dim3 lgrid(static_cast<unsigned>((st->n_envs + per_block - 1) / per_block));
+    const size_t llds = sc_level_lds_bytes(cfg);
+    const int G = cfg->group, IB = cfg->inbox_size;
+    switch (sc_maxd_bucket(cfg->max_dests)) {
+      case 2: hipLaunchKernelGGL(sc_level_kernel<2>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
+      case 4: hipLaunchKernelGGL(sc_level_kernel<4>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
+      case 8: hipLaunchKernelGGL(sc_level_kernel<8>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
+      case 16: hipLaunchKernelGGL(sc_level_kernel<16>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
+      default: hipLaunchKernelGGL(sc_level_kernel<32>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
+    }
+  } else if (cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST) {
+    return fail(SCG_ERR_INVALID, "lane kernel needs the env-fastest layout");
+  } else if (lds <= kScLdsMax) {
     switch (sc_maxd_bucket(cfg->max_dests)) {
       case 2: hipLaunchKernelGGL(sc_step_lds_kernel<2>, grid, dim3(kScBlock), lds, s, a); break;
       case 4: hipLaunchKernelGGL(sc_step_lds_kernel<4>, grid, dim3(kScBlock), lds, s, a); break;

@@ -114,17 +114,29 @@ __host__ __device__ __forceinline__ void sc_push(const ScCtx& c, ScEnv& e, int n
   if (!py_heappush(sc_heap(c, e, node, p), sz, c.H, HeapEntry{he_pack(time, amount.k), amount.v})) e.overflow = 1;
 }
 
-// SC_Node.reset (:402-412): stock back to initial_stock, heaps re-seeded at times 1..k
-// (initial_supply entries first, then initial_shipments, each pushed with heappush).
-__host__ __device__ inline void sc_reset_env(const ScCtx& c, ScEnv& e) {
-  for (int i = 0; i < c.n_nodes; ++i) {
-    const scg_sc_node& nd = c.nodes[i];
-    for (int p = 0; p < c.P; ++p) {
-      sc_stock(c, e, i, p) = static_cast<double>(nd.initial_stock[p]);
-      sc_size(c, e, i, p) = 0;
-      for (int j = 0; j < nd.n_init[p]; ++j) sc_push(c, e, i, p, nd.init_time[p][j], pyint(nd.init_amount[p][j]));
-    }
+// Where SHIP pushes go (:347): straight into the destination heap when one lane walks the
+// whole chain in node order (sc_step_env), or into a level inbox that the destination's
+// lane drains in source order before its own act (scg_supplychain_level.h).
+struct DirectPush {
+  __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv& e, int /*src*/, int dest, int p, int32_t time,
+                                                Num amount) const {
+    sc_push(c, e, dest, p, time, amount);
   }
+};
+
+// SC_Node.reset (:402-412) for one (node, product): stock back to initial_stock, the heap
+// re-seeded at times 1..k (initial_supply entries first, then initial_shipments, each
+// pushed with heappush). Heaps are independent, so any lane may reset any of them.
+__host__ __device__ inline void sc_reset_heap(const ScCtx& c, ScEnv& e, int i, int p) {
+  const scg_sc_node& nd = c.nodes[i];
+  sc_stock(c, e, i, p) = static_cast<double>(nd.initial_stock[p]);
+  sc_size(c, e, i, p) = 0;
+  for (int j = 0; j < nd.n_init[p]; ++j) sc_push(c, e, i, p, nd.init_time[p][j], pyint(nd.init_amount[p][j]));
+}
+
+__host__ __device__ inline void sc_reset_env(const ScCtx& c, ScEnv& e) {
+  for (int i = 0; i < c.n_nodes; ++i)
+    for (int p = 0; p < c.P; ++p) sc_reset_heap(c, e, i, p);
 }
 
 // MAXD scalars with their NumPy kinds, the kinds packed 4 bits per entry so an unrolled
@@ -210,9 +222,9 @@ __host__ __device__ __forceinline__ Num sc_action(const float* raw, int k) {
 
 // SC_Node.act (:208-396) for node `ni` at time t; `act` = this env's raw float32 action
 // row. Returns the node's cost with its NumPy kind. MAXD bounds the node's destinations.
-template <int MAXD>
+template <int MAXD, class Push = DirectPush>
 __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& ltc, WordCache& dmc, int ni,
-                                           const float* act, int t) {
+                                           const float* act, int t, const Push& push = Push()) {
   const scg_sc_node& nd = c.nodes[ni];
   const int P = c.P;
   Num cost = pyint(0);
@@ -297,7 +309,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
           }
           leaving = np_add(leaving, o);
           if (np_lt(pyint(0), snt))
-            sc_push(c, e, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
+            push.ship(c, e, ni, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
           ship_cost = np_add(ship_cost, np_mul(snt, pyint(nd.dest_costs[p][i])));
         }
         double& st = sc_stock(c, e, ni, p);
@@ -336,49 +348,66 @@ __host__ __device__ inline double sc_step_env(const ScCtx& c, ScEnv& e, const fl
 
 // Observation at time t (:762-791): normalised next demands, per node stock share and
 // in-transit bins (storage-order walk, :445-461), time to go; 2x-1 clipped to [-1, 1].
+// Element o of the row is written by out(o, value); the pieces below write disjoint
+// elements, so lanes may emit different pieces of one row in any order.
+__host__ __device__ __forceinline__ double sc_obs_norm(double x) {
+  const double y = x * 2.0 - 1.0;
+  return y < -1.0 ? -1.0 : (y > 1.0 ? 1.0 : y);
+}
+
+// demand element k = r * P + p
+template <class Sink>
+__host__ __device__ inline void sc_observe_demand(const ScCtx& c, const ScEnv& e, int t, int k, Sink& out) {
+  WordCache dmc{0, U4{0, 0, 0, 0}, false};
+  const double range = static_cast<double>(c.hi - c.lo);
+  out(k, sc_obs_norm(static_cast<double>(sc_demand(c, e, dmc, t, k / c.P, k % c.P) - c.lo) / range));
+}
+
+// node i, product p: stock share, then avg_leadtime in-transit bins
+template <class Sink>
+__host__ __device__ inline void sc_observe_heap(const ScCtx& c, const ScEnv& e, int t, int i, int p, Sink& out) {
+  const scg_sc_node& nd = c.nodes[i];
+  const int nb = c.avg_lt;
+  const int base = c.R * c.P + i * (c.P + c.P * nb);
+  out(base + p, sc_obs_norm(sc_stock(c, e, i, p) / static_cast<double>(nd.stock_capacity[p])));
+  int o = base + c.P + p * nb;
+  const int first = t + 1, last = t + c.avg_lt;
+  const HeapView h = sc_heap(c, e, i, p);
+  const int32_t sz = sc_size(c, e, i, p);
+  if (sz == 0) {
+    for (int b = first; b <= last; ++b) out(o++, sc_obs_norm(0.0));
+    return;
+  }
+  int k = 0;
+  for (int when = first; when < last; ++when) {
+    Num bin = pyint(0);
+    while (k < sz && h.time_at(k) == when) {
+      const HeapEntry en = h.get(k);
+      bin = np_add(bin, Num{en.v, he_kind(en.tk)});
+      ++k;
+    }
+    out(o++, sc_obs_norm(np_div(bin, pyint(nd.max_ship[p])).v));
+  }
+  Num bin = pyint(0);
+  while (k < sz) {
+    const HeapEntry en = h.get(k);
+    bin = np_add(bin, Num{en.v, he_kind(en.tk)});
+    ++k;
+  }
+  out(o, sc_obs_norm(np_div(bin, pyint(nd.max_ship[p] * (c.max_lt - (last - first)))).v));
+}
+
+template <class Sink>
+__host__ __device__ inline void sc_observe_tail(const ScCtx& c, int t, Sink& out) {
+  out(c.O - 1, sc_obs_norm(static_cast<double>(c.T - t) / static_cast<double>(c.T)));
+}
+
 template <class Sink>
 __host__ __device__ inline void sc_observe(const ScCtx& c, ScEnv& e, int t, Sink& out) {
-  int o = 0;
-  WordCache dmc{0, U4{0, 0, 0, 0}, false};
-  auto emit = [&](double x) {
-    double y = x * 2.0 - 1.0;
-    y = y < -1.0 ? -1.0 : (y > 1.0 ? 1.0 : y);
-    out(o++, y);
-  };
-  const double range = static_cast<double>(c.hi - c.lo);
-  for (int r = 0; r < c.R; ++r)
-    for (int p = 0; p < c.P; ++p) emit(static_cast<double>(sc_demand(c, e, dmc, t, r, p) - c.lo) / range);
-  const int first = t + 1, last = t + c.avg_lt;
-  for (int i = 0; i < c.n_nodes; ++i) {
-    const scg_sc_node& nd = c.nodes[i];
-    for (int p = 0; p < c.P; ++p) emit(sc_stock(c, e, i, p) / static_cast<double>(nd.stock_capacity[p]));
-    for (int p = 0; p < c.P; ++p) {
-      const HeapView h = sc_heap(c, e, i, p);
-      const int32_t sz = sc_size(c, e, i, p);
-      if (sz == 0) {
-        for (int b = first; b <= last; ++b) emit(0.0);
-        continue;
-      }
-      int k = 0;
-      for (int when = first; when < last; ++when) {
-        Num bin = pyint(0);
-        while (k < sz && h.time_at(k) == when) {
-          const HeapEntry en = h.get(k);
-          bin = np_add(bin, Num{en.v, he_kind(en.tk)});
-          ++k;
-        }
-        emit(np_div(bin, pyint(nd.max_ship[p])).v);
-      }
-      Num bin = pyint(0);
-      while (k < sz) {
-        const HeapEntry en = h.get(k);
-        bin = np_add(bin, Num{en.v, he_kind(en.tk)});
-        ++k;
-      }
-      emit(np_div(bin, pyint(nd.max_ship[p] * (c.max_lt - (last - first)))).v);
-    }
-  }
-  emit(static_cast<double>(c.T - t) / static_cast<double>(c.T));
+  for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, e, t, k, out);
+  for (int i = 0; i < c.n_nodes; ++i)
+    for (int p = 0; p < c.P; ++p) sc_observe_heap(c, e, t, i, p, out);
+  sc_observe_tail(c, t, out);
 }
 
 }  // namespace scg

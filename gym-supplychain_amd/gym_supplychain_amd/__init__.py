@@ -31,7 +31,8 @@ ENV_IDS = {
     "sc-Nperstage-multiproduct-v0": "gym_supplychain_amd.envs:SupplyChainNPerStage",
     "sc-2perstage-multiproduct-inccosts-v0": "gym_supplychain_amd.envs:SupplyChainMultiProduct_IncreasingCosts",
 }
-_VEC_KEYS = ("seed", "device", "env_offset", "auto_reset", "obs_dtype", "track_returns")
+_VEC_KEYS = ("seed", "device", "env_offset", "auto_reset", "obs_dtype", "track_returns", "kernel", "demand_table",
+             "leadtime_table")
 
 
 def _sc_vec(builder):

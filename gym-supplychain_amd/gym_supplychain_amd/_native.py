@@ -100,6 +100,9 @@ SC_MAX_PRODUCTS = 8
 SC_MAX_DESTS = 32
 SC_MAX_INIT = 16
 SC_MAX_NODES = 256
+SC_MAX_LEVELS = 16
+SC_KERNEL_AUTO, SC_KERNEL_LANE, SC_KERNEL_LEVEL = 0, 1, 2
+SC_LAYOUT_ENV_FASTEST, SC_LAYOUT_ENV_MAJOR = 0, 1
 SCG_STREAM_SC_DEMAND = 2
 SCG_STREAM_SC_LEADTIME = 3
 
@@ -130,7 +133,9 @@ class ScConfig(ctypes.Structure):
         "exceeded_stock_capacity_cost", "exceeded_process_capacity_cost", "exceeded_ship_capacity_cost",
         "heap_capacity", "leadtime_poisson_len", "obs_f64", "max_dests")] + [
         ("nodes", ctypes.c_void_p), ("leadtime_poisson", ctypes.c_void_p), ("demand_table", ctypes.c_void_p),
-        ("leadtime_table", ctypes.c_void_p)]
+        ("leadtime_table", ctypes.c_void_p)] + [
+        (f, ctypes.c_int32) for f in ("kernel", "layout", "group", "n_levels")] + [
+        ("level_start", ctypes.c_int32 * (SC_MAX_LEVELS + 1)), ("inbox_size", ctypes.c_int32)]
 
 
 class ScState(ctypes.Structure):

@@ -207,10 +207,16 @@ class SupplyChainVecEnv:
     demand_table / leadtime_table: optional device int32 tensors [N, T+1, R, P] /
     [N, T, n_lt] used for every episode instead of the Philox draws (e.g. to replay the
     reference's RandomState episodes exactly).
+    kernel: "auto" (the level-parallel kernel whenever the chain has a level schedule,
+    DESIGN.md §6), "level" or "lane" (one lane walks one env's whole chain). Both give the
+    same results; the state layout follows the kernel.
     """
 
+    _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL}
+
     def __init__(self, n_envs, nodes_info=None, spec=None, seed=0, device=None, env_offset=0, auto_reset=True,
-                 obs_dtype=torch.float32, track_returns=True, demand_table=None, leadtime_table=None, **kwargs):
+                 obs_dtype=torch.float32, track_returns=True, demand_table=None, leadtime_table=None, kernel="auto",
+                 **kwargs):
         if spec is None:
             if nodes_info is None:
                 raise ValueError("pass nodes_info (+ SupplyChainEnv keywords) or a SupplyChainSpec")
@@ -244,7 +250,12 @@ class SupplyChainVecEnv:
         for k, v in spec.penalties.items():
             setattr(c, k, v)
         c.obs_f64 = int(obs_dtype == torch.float64)
+        if kernel not in self._KERNELS:
+            raise ValueError(f"kernel must be one of {sorted(self._KERNELS)}, got {kernel!r}")
+        c.kernel = self._KERNELS[kernel]
         nat.check(nat.lib.scg_sc_prepare(ctypes.byref(c), host_nodes))
+        self.kernel = "level" if c.kernel == nat.SC_KERNEL_LEVEL else "lane"
+        self._env_major = c.layout == nat.SC_LAYOUT_ENV_MAJOR
         if (c.n_actions, c.n_obs, c.n_leadtimes) != (spec.n_actions, spec.n_obs, spec.n_leadtimes):
             raise RuntimeError("host/library disagree on the chain's action/observation sizes")
         self._node_bytes = torch.frombuffer(bytearray(bytes(host_nodes)), dtype=torch.uint8).to(self.device)
@@ -273,10 +284,16 @@ class SupplyChainVecEnv:
         self.n_actions, self.n_obs, self.heap_capacity = c.n_actions, c.n_obs, c.heap_capacity
         NP, H = NN * P, c.heap_capacity
         dev = self.device
-        self._stock = torch.zeros((NP, n_envs), dtype=torch.float64, device=dev)
-        self._heap_tk = torch.zeros((NP, H, n_envs), dtype=torch.int32, device=dev)
-        self._heap_val = torch.zeros((NP, H, n_envs), dtype=torch.float64, device=dev)
-        self._heap_size = torch.zeros((NP, n_envs), dtype=torch.int32, device=dev)
+        if self._env_major:  # [N][NP], [N][NP][H]: one env's chain is one contiguous block
+            self._stock = torch.zeros((n_envs, NP), dtype=torch.float64, device=dev)
+            self._heap_tk = torch.zeros((n_envs, NP, H), dtype=torch.int32, device=dev)
+            self._heap_val = torch.zeros((n_envs, NP, H), dtype=torch.float64, device=dev)
+            self._heap_size = torch.zeros((n_envs, NP), dtype=torch.int32, device=dev)
+        else:  # env-fastest: lanes of a wave touching one slot read one contiguous row
+            self._stock = torch.zeros((NP, n_envs), dtype=torch.float64, device=dev)
+            self._heap_tk = torch.zeros((NP, H, n_envs), dtype=torch.int32, device=dev)
+            self._heap_val = torch.zeros((NP, H, n_envs), dtype=torch.float64, device=dev)
+            self._heap_size = torch.zeros((NP, n_envs), dtype=torch.int32, device=dev)
         self._err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None
         self._final_ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None
@@ -381,6 +398,8 @@ class SupplyChainVecEnv:
     @property
     def stock(self):
         """[N, nodes, P] float64 view of every node's stock."""
+        if self._env_major:
+            return self._stock.view(self.n_envs, len(self.spec.nodes), self.spec.P)
         return self._stock.view(len(self.spec.nodes), self.spec.P, self.n_envs).permute(2, 0, 1)
 
     @property
@@ -395,9 +414,13 @@ class SupplyChainVecEnv:
         """In-transit heaps of one env as the reference's shipments_by_prod lists
         [node][product] -> [(time, amount), ...] in storage order."""
         P = self.spec.P
-        tk = self._heap_tk[:, :, env].cpu().numpy()
-        val = self._heap_val[:, :, env].cpu().numpy()
-        size = self._heap_size[:, env].cpu().numpy()
+        if self._env_major:
+            tk, val, size = (self._heap_tk[env].cpu().numpy(), self._heap_val[env].cpu().numpy(),
+                             self._heap_size[env].cpu().numpy())
+        else:
+            tk = self._heap_tk[:, :, env].cpu().numpy()
+            val = self._heap_val[:, :, env].cpu().numpy()
+            size = self._heap_size[:, env].cpu().numpy()
         out = []
         for i in range(len(self.spec.nodes)):
             out.append([[(int(tk[i * P + p, j]) >> 3, float(val[i * P + p, j])) for j in range(size[i * P + p])]

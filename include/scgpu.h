@@ -216,6 +216,14 @@ SCG_API int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, 
 #define SCG_SC_MAX_DESTS 32
 #define SCG_SC_MAX_INIT 16
 #define SCG_SC_MAX_NODES 256
+#define SCG_SC_MAX_LEVELS 16
+
+/* SupplyChain kernels (scg_sc_config.kernel) and the state layouts they use. */
+#define SCG_SC_KERNEL_AUTO 0
+#define SCG_SC_KERNEL_LANE 1  /* one lane walks one env's whole chain; env-fastest state       */
+#define SCG_SC_KERNEL_LEVEL 2 /* a lane group per env, one lane per node of a level; env-major */
+#define SCG_SC_LAYOUT_ENV_FASTEST 0 /* stock [NP][N], heaps [NP][H][N], sizes [NP][N]          */
+#define SCG_SC_LAYOUT_ENV_MAJOR 1   /* stock [N][NP], heaps [N][NP][H], sizes [N][NP]          */
 #define SCG_STREAM_SC_DEMAND 2u
 #define SCG_STREAM_SC_LEADTIME 3u
 
@@ -264,9 +272,20 @@ typedef struct scg_sc_config {
   const int32_t* demand_table;  /* DEVICE [N][T+1][R][P] caller tables instead of Philox    */
                                 /* (NULL = draw; e.g. to replay RandomState episodes)       */
   const int32_t* leadtime_table;/* DEVICE [N][T][n_leadtimes] likewise (stochastic only)    */
+  /* Kernel choice (in: SCG_SC_KERNEL_*, 0 = auto; out: the kernel scg_sc_step launches) and
+   * what scg_sc_prepare derives for it: the state layout, lanes per env and the level
+   * schedule (levels are runs of consecutive nodes; every shipment goes from a level to
+   * the next one, so a level's nodes never depend on each other within a step). */
+  int32_t kernel;
+  int32_t layout;               /* out: SCG_SC_LAYOUT_*                                     */
+  int32_t group;                /* out: lanes per env (level kernel)                        */
+  int32_t n_levels;             /* out: 0 when the chain has no such schedule               */
+  int32_t level_start[SCG_SC_MAX_LEVELS + 1];
+  int32_t inbox_size;           /* out: shipment inbox entries per env (level kernel)       */
 } scg_sc_config;
 
-/* Batch state. NP = n_nodes * n_products; per-env arrays are env-fastest. */
+/* Batch state. NP = n_nodes * n_products; per-env arrays follow cfg->layout (shapes below
+ * are the env-fastest ones; env-major puts the env index first). */
 typedef struct scg_sc_state {
   int64_t n_envs;
   int64_t env_offset;

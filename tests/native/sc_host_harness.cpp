@@ -4,12 +4,27 @@
 // product: libscgpu.so has no CPU path, and this library is built by the tests only.
 #include <cstring>
 
-#include "scg_supplychain_core.h"
+#include <vector>
 
-extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
-                           uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
-                           double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
-                           int32_t* heap_size) {
+#include "scg_supplychain_core.h"
+#include "scg_supplychain_level.h"
+
+namespace {
+// The level kernel's schedule on the host: a phase runs the lane body for every lane of
+// the group in turn (the device runs them concurrently, then a barrier).
+struct HostSched {
+  int G;
+  template <class F>
+  void phase(F&& f) {
+    for (int s = 0; s < G; ++s) f(s);
+  }
+};
+}  // namespace
+
+static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                        uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
+                        double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
+                        int32_t* heap_size) {
   scg::ScCtx c;
   std::memset(&c, 0, sizeof(c));
   c.nodes = nodes;
@@ -58,6 +73,31 @@ extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, c
     scg::ScEnv et{stock + t * NP, heap_tk + static_cast<int64_t>(t) * NP * c.H,
                   heap_val + static_cast<int64_t>(t) * NP * c.H, heap_size + t * NP, 1, 1, env_id, 0, episode, 0};
     const float* a = actions + static_cast<int64_t>(t - 1) * c.A;
+    if (level) {  // sc_level_kernel's phases, lanes in turn
+      scg::ScLevels lv;
+      lv.n = cfg->n_levels;
+      for (int l = 0; l <= SCG_SC_MAX_LEVELS; ++l) lv.start[l] = cfg->level_start[l];
+      std::vector<scg::Num> cost(c.n_nodes);
+      std::vector<int32_t> in_tk(cfg->inbox_size, 0x7fffffff);  // garbage until a node writes its row
+      std::vector<double> in_val(cfg->inbox_size, -1.0);
+      scg::ScLevelEnv x{et, in_tk.data(), in_val.data(), cost.data(), a};
+      HostSched sch{cfg->group};
+      double r = 0.0;
+      switch (scg::sc_maxd_bucket(cfg->max_dests)) {
+        case 2: r = scg::sc_level_step<2>(c, lv, x, t, sch); break;
+        case 4: r = scg::sc_level_step<4>(c, lv, x, t, sch); break;
+        case 8: r = scg::sc_level_step<8>(c, lv, x, t, sch); break;
+        case 16: r = scg::sc_level_step<16>(c, lv, x, t, sch); break;
+        default: r = scg::sc_level_step<32>(c, lv, x, t, sch); break;
+      }
+      rewards[t - 1] = r;
+      et.overflow |= x.e.overflow;
+      double* row = obs + static_cast<int64_t>(t) * c.O;
+      auto out = [row](int o, double v) { row[o] = v; };
+      for (int s2 = 0; s2 < cfg->group; ++s2) scg::sc_level_observe_lane(c, x.e, t, out, s2, cfg->group);
+      if (et.overflow) return 1;
+      continue;
+    }
     switch (scg::sc_maxd_bucket(cfg->max_dests)) {  // the instantiation the GPU launch picks
       case 2: rewards[t - 1] = scg::sc_step_env<2>(c, et, a, t); break;
       case 4: rewards[t - 1] = scg::sc_step_env<4>(c, et, a, t); break;
@@ -70,4 +110,19 @@ extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, c
     if (et.overflow) return 1;
   }
   return e.overflow;
+}
+
+extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr, uint64_t seed,
+                           uint32_t env_id, uint32_t episode, int32_t steps, const float* actions, double* obs,
+                           double* rewards, double* stock, int32_t* heap_tk, double* heap_val, int32_t* heap_size) {
+  return episode_impl(false, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+                      heap_val, heap_size);
+}
+
+extern "C" int sch_episode_level(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                                 uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
+                                 double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
+                                 int32_t* heap_size) {
+  return episode_impl(true, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+                      heap_val, heap_size);
 }

@@ -23,10 +23,11 @@ def build():
                         "-o", OUT, SRC], check=True)
     lib = ctypes.CDLL(OUT)
     lib.sch_episode.restype = ctypes.c_int
+    lib.sch_episode_level.restype = ctypes.c_int
     return lib
 
 
-def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions):
+def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=False):
     """Reset + len(actions) steps of one env; returns obs [T+1, O], rewards [T],
     stock [T+1, NP], heaps (tk, val, size) per snapshot."""
     T = actions.shape[0]
@@ -41,7 +42,8 @@ def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions):
     thr = np.asarray(lt_thr if lt_thr is not None else [0], dtype=np.uint32)
     acts = np.ascontiguousarray(actions, dtype=np.float32)
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    rc = lib.sch_episode(ctypes.byref(cfg), nodes, p(thr), ctypes.c_uint64(seed), ctypes.c_uint32(env_id),
+    fn = lib.sch_episode_level if level else lib.sch_episode
+    rc = fn(ctypes.byref(cfg), nodes, p(thr), ctypes.c_uint64(seed), ctypes.c_uint32(env_id),
                          ctypes.c_uint32(episode), ctypes.c_int32(T), p(acts), p(obs), p(rew), p(stock), p(tk),
                          p(val), p(size))
     return rc, obs, rew, stock, (tk, val, size)

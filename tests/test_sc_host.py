@@ -18,7 +18,7 @@ def harness():
     return native_harness.build()
 
 
-def _setup(g):
+def _setup(g, kernel=0):
     import ctypes
     from gym_supplychain_amd import _native as nat
     from gym_supplychain_amd.envs import SupplyChainSpec
@@ -36,21 +36,26 @@ def _setup(g):
     if spec.stochastic_leadtimes:
         thr = nat.poisson_table(spec.avg_leadtime - 1)
         c.leadtime_poisson_len = len(thr)
+    c.kernel = kernel
     assert nat.lib.scg_sc_prepare(ctypes.byref(c), nodes) == 0, nat.last_error()
     return spec, c, nodes, thr
 
 
+@pytest.mark.parametrize("kernel", ["lane", "level"])
 @pytest.mark.parametrize("name", CASES)
-def test_host_build_of_kernel_body_matches_reference(harness, name):
+def test_host_build_of_kernel_body_matches_reference(harness, name, kernel):
+    """Both kernels' step bodies: the lane kernel's serial chain walk and the level
+    kernel's phases (scg_supplychain_level.h) with the group's lanes run in turn."""
     import native_harness
+    from gym_supplychain_amd import _native as nat
     g = load_sc(name)
     meta = g["meta"]
-    spec, c, nodes, thr = _setup(g)
+    spec, c, nodes, thr = _setup(g, nat.SC_KERNEL_LANE if kernel == "lane" else nat.SC_KERNEL_LEVEL)
     N = g["obs"].shape[1]
     P, H = spec.P, c.heap_capacity
     for n in range(N):
         rc, obs, rew, stock, (tk, val, size) = native_harness.run_episode(harness, c, nodes, thr, meta["seed"], n, 0,
-                                                                           g["actions"][:, n])
+                                                                           g["actions"][:, n], kernel == "level")
         assert rc == 0
         assert np.array_equal(obs, g["obs"][:, n]), name
         assert np.array_equal(rew, g["reward"][:, n]), name

@@ -77,13 +77,14 @@ def cpu_baseline(name, budget=1.5, max_procs=16):
                       f"oracle.supplychain.SupplyChainOracle; {steps} env-steps"}
 
 
-def run(name, steps, warmup, n_envs, cpu):
+def run(name, steps, warmup, n_envs, cpu, kernel="auto"):
     import torch
     import gym_supplychain_amd as gsa
     sc = SCENARIOS[name]
     N = n_envs or sc["n_envs"]
     dev = torch.device("cuda", 0)
-    env = gsa.make_vec(sc["env_id"], N, seed=0, device=dev, obs_dtype=torch.float32, auto_reset=True, **sc["kwargs"])
+    env = gsa.make_vec(sc["env_id"], N, seed=0, device=dev, obs_dtype=torch.float32, auto_reset=True, kernel=kernel,
+                       **sc["kwargs"])
     gen = torch.Generator(device=dev).manual_seed(0)
     pool = [torch.rand((N, env.n_actions), generator=gen, device=dev) * 2 - 1 for _ in range(4)]
     env.reset()
@@ -108,9 +109,11 @@ def run(name, steps, warmup, n_envs, cpu):
             "ms_per_step": wall * 1e3 / steps, "higher_is_better": True, "dtype": "f32 actions/obs, f64 state",
             "data": "synthetic: uniform demand drawn on device (Philox4x32-10), U[-1,1] float32 actions",
             "config": {"workload": f"{sc['env_id']} step() (BASELINE {sc['baseline_cfg']})", "n_envs": N,
+                       "kernel": env.kernel,
                        "n_actions": env.n_actions, "n_obs": env.n_obs, "heap_capacity": env.heap_capacity},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "scg::sc_step_kernel",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "scg::sc_level_kernel" if env.kernel == "level" else "scg::sc_step(_lds)_kernel",
                          "avg_kernel_us": kern_s * 1e6, "bytes_per_env_step": bpe}}
     del env, pool
     torch.cuda.empty_cache()
@@ -126,9 +129,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "both"])
     a = ap.parse_args()
+    kernels = ["lane", "level"] if a.kernel == "both" else [a.kernel]
     for name in (["2perstage", "ntom"] if a.scenario == "both" else [a.scenario]):
-        run(name, a.steps, a.warmup, a.envs, not a.no_cpu_baseline)
+        for k in kernels:
+            run(name, a.steps, a.warmup, a.envs, not a.no_cpu_baseline and k == kernels[-1], k)
 
 
 if __name__ == "__main__":
