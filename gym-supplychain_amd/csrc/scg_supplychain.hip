@@ -192,24 +192,65 @@ struct DevSched {
   }
 };
 
-__device__ __forceinline__ size_t level_env_lds(const ScCtx& c, int inbox) {
-  return ((static_cast<size_t>(c.n_nodes) * sizeof(Num) + static_cast<size_t>(inbox) * 12 + 15) / 16) * 16;
+// LDS of one env in the level kernel: node costs and the inbox, plus — when staged — the
+// env's whole mutable state (heaps, sizes, stock), so every heap walk of the step runs at
+// LDS latency. Doubles first, then 32-bit arrays, each 16-byte aligned.
+struct LevelLds {
+  size_t cost, in_val, hval, stock, in_tk, htk, hsize, total;
+};
+
+__host__ __device__ __forceinline__ size_t a16(size_t b) { return (b + 15) / 16 * 16; }
+
+__host__ __device__ inline LevelLds level_lds(int n_nodes, int P, int H, int inbox, bool staged) {
+  const size_t NP = static_cast<size_t>(n_nodes) * P;
+  LevelLds l;
+  l.cost = 0;
+  l.in_val = l.cost + a16(static_cast<size_t>(n_nodes) * sizeof(Num));
+  l.hval = l.in_val + a16(static_cast<size_t>(inbox) * 8);
+  l.stock = l.hval + (staged ? a16(NP * H * 8) : 0);
+  l.in_tk = l.stock + (staged ? a16(NP * 8) : 0);
+  l.htk = l.in_tk + a16(static_cast<size_t>(inbox) * 4);
+  l.hsize = l.htk + (staged ? a16(NP * H * 4) : 0);
+  l.total = l.hsize + (staged ? a16(NP * 4) : 0);
+  return l;
 }
 
-template <int MAXD>
+template <int MAXD, bool STAGED>
 __global__ __launch_bounds__(kScBlock) void sc_level_kernel(const ScArgs a, const ScLevels lv, int G, int inbox) {
   extern __shared__ __align__(16) unsigned char smem[];
   const ScCtx& c = a.c;
   const int g = threadIdx.x / G;
   const int64_t n = static_cast<int64_t>(blockIdx.x) * (kScBlock / G) + g;
   DevSched sch{G, static_cast<int>(threadIdx.x) % G, n < a.n};
-  unsigned char* mine = smem + g * level_env_lds(c, inbox);
+  const LevelLds L = level_lds(c.n_nodes, c.P, c.H, inbox, STAGED);
+  unsigned char* mine = smem + g * L.total;
   ScLevelEnv x;
-  x.cost = reinterpret_cast<Num*>(mine);
-  x.in_val = reinterpret_cast<double*>(mine + c.n_nodes * sizeof(Num));
-  x.in_tk = reinterpret_cast<int32_t*>(x.in_val + inbox);
+  x.cost = reinterpret_cast<Num*>(mine + L.cost);
+  x.in_val = reinterpret_cast<double*>(mine + L.in_val);
+  x.in_tk = reinterpret_cast<int32_t*>(mine + L.in_tk);
   const int64_t m = sch.live ? n : 0;  // idle groups (tail block) only join the barriers
-  x.e = env_view(a, m, a.episode);
+  const ScEnv ge = env_view(a, m, a.episode);  // the env's block in HBM
+  const int NP = c.n_nodes * c.P, H = c.H;
+  if (STAGED) {  // copy in the live part of the env's state, coalesced over the group
+    x.e = ScEnv{reinterpret_cast<double*>(mine + L.stock), reinterpret_cast<int32_t*>(mine + L.htk),
+                reinterpret_cast<double*>(mine + L.hval), reinterpret_cast<int32_t*>(mine + L.hsize), 1, 1,
+                ge.env_id, ge.local, ge.episode, 0};
+    sch.phase([&](int s) {
+      for (int k = s; k < NP; k += G) {
+        x.e.size[k] = ge.size[k];
+        x.e.stock[k] = ge.stock[k];
+      }
+    });
+    sch.phase([&](int s) {
+      for (int q = s; q < NP * H; q += G)
+        if (q % H < x.e.size[q / H]) {
+          x.e.tk[q] = ge.tk[q];
+          x.e.val[q] = ge.val[q];
+        }
+    });
+  } else {
+    x.e = ge;
+  }
   x.act = a.act + m * c.A;
   const double reward = sc_level_step<MAXD>(c, lv, x, a.t, sch);
   const bool terminal = a.flags & 1;
@@ -232,6 +273,19 @@ __global__ __launch_bounds__(kScBlock) void sc_level_kernel(const ScArgs a, cons
     sch.phase([&](int s) {
       sc_level_observe_lane(c, x.e, a.t, out, s, G);
       if (terminal && a.term_obs) sc_level_observe_lane(c, x.e, a.t, tout, s, G);
+    });
+  }
+  if (STAGED) {  // copy the live part back
+    sch.phase([&](int s) {
+      for (int k = s; k < NP; k += G) {
+        ge.size[k] = x.e.size[k];
+        ge.stock[k] = x.e.stock[k];
+      }
+      for (int q = s; q < NP * H; q += G)
+        if (q % H < x.e.size[q / H]) {
+          ge.tk[q] = x.e.tk[q];
+          ge.val[q] = x.e.val[q];
+        }
     });
   }
   if (sch.live && x.e.overflow) atomicOr(a.err, 1);
@@ -320,10 +374,10 @@ dim3 sc_grid(int64_t n) { return dim3(static_cast<unsigned>((n + kScBlock - 1) /
 // LDS the staged step kernel needs per 64-env block; staged only while >= 2 blocks fit a CU.
 constexpr size_t kScLdsMax = 64 * 1024;
 
-// LDS of the level kernel per block: (64 / G) envs x (node costs + inbox), as level_env_lds.
+// LDS of the level kernel per block: (64 / G) envs x level_lds.
 size_t sc_level_lds_bytes(const scg_sc_config* cfg) {
-  const size_t per_env = ((static_cast<size_t>(cfg->n_nodes) * sizeof(Num) + static_cast<size_t>(cfg->inbox_size) * 12 + 15) / 16) * 16;
-  return static_cast<size_t>(kScBlock / cfg->group) * per_env;
+  return static_cast<size_t>(kScBlock / cfg->group) *
+         level_lds(cfg->n_nodes, cfg->n_products, cfg->heap_capacity, cfg->inbox_size, cfg->level_staged).total;
 }
 
 // The level schedule of a chain (scg_supplychain_level.h), or false when it has none:
@@ -363,6 +417,14 @@ bool sc_level_schedule(scg_sc_config* cfg, const scg_sc_node* nodes) {
   cfg->n_levels = L;
   cfg->group = G;
   cfg->inbox_size = inbox;
+  // Stage each env's state in LDS when a block's share fits; widen the group (fewer envs
+  // per block) until it does.
+  cfg->level_staged = 1;
+  while (sc_level_lds_bytes(cfg) > kScLdsMax && cfg->group < kScBlock) cfg->group *= 2;
+  if (sc_level_lds_bytes(cfg) > kScLdsMax) {
+    cfg->level_staged = 0;
+    cfg->group = G;
+  }
   return sc_level_lds_bytes(cfg) <= kScLdsMax;
 }
 size_t sc_lds_bytes(const scg_sc_config* cfg) {
@@ -466,6 +528,7 @@ int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
   cfg->n_levels = 0;
   cfg->group = 1;
   cfg->inbox_size = 0;
+  cfg->level_staged = 0;
   const bool levels = want != SCG_SC_KERNEL_LANE && sc_level_schedule(cfg, nodes);
   if (want == SCG_SC_KERNEL_LEVEL && !levels)
     return fail(SCG_ERR_INVALID, "the chain has no level schedule (shipments must go to the next run of nodes)");
@@ -515,13 +578,19 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
     const dim3 lgrid(static_cast<unsigned>((st->n_envs + per_block - 1) / per_block));
     const size_t llds = sc_level_lds_bytes(cfg);
     const int G = cfg->group, IB = cfg->inbox_size;
+#define SCG_LEVEL_LAUNCH(D)                                                                               \
+  if (cfg->level_staged)                                                                                  \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_level_kernel<D, true>), lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); \
+  else                                                                                                    \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_level_kernel<D, false>), lgrid, dim3(kScBlock), llds, s, a, lv, G, IB)
     switch (sc_maxd_bucket(cfg->max_dests)) {
-      case 2: hipLaunchKernelGGL(sc_level_kernel<2>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
-      case 4: hipLaunchKernelGGL(sc_level_kernel<4>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
-      case 8: hipLaunchKernelGGL(sc_level_kernel<8>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
-      case 16: hipLaunchKernelGGL(sc_level_kernel<16>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
-      default: hipLaunchKernelGGL(sc_level_kernel<32>, lgrid, dim3(kScBlock), llds, s, a, lv, G, IB); break;
+      case 2: SCG_LEVEL_LAUNCH(2); break;
+      case 4: SCG_LEVEL_LAUNCH(4); break;
+      case 8: SCG_LEVEL_LAUNCH(8); break;
+      case 16: SCG_LEVEL_LAUNCH(16); break;
+      default: SCG_LEVEL_LAUNCH(32); break;
     }
+#undef SCG_LEVEL_LAUNCH
   } else if (cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST) {
     return fail(SCG_ERR_INVALID, "lane kernel needs the env-fastest layout");
   } else if (lds <= kScLdsMax) {

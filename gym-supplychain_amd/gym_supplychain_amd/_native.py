@@ -135,7 +135,8 @@ class ScConfig(ctypes.Structure):
         ("nodes", ctypes.c_void_p), ("leadtime_poisson", ctypes.c_void_p), ("demand_table", ctypes.c_void_p),
         ("leadtime_table", ctypes.c_void_p)] + [
         (f, ctypes.c_int32) for f in ("kernel", "layout", "group", "n_levels")] + [
-        ("level_start", ctypes.c_int32 * (SC_MAX_LEVELS + 1)), ("inbox_size", ctypes.c_int32)]
+        ("level_start", ctypes.c_int32 * (SC_MAX_LEVELS + 1)), ("inbox_size", ctypes.c_int32),
+        ("level_staged", ctypes.c_int32)]
 
 
 class ScState(ctypes.Structure):

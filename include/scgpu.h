@@ -282,6 +282,7 @@ typedef struct scg_sc_config {
   int32_t n_levels;             /* out: 0 when the chain has no such schedule               */
   int32_t level_start[SCG_SC_MAX_LEVELS + 1];
   int32_t inbox_size;           /* out: shipment inbox entries per env (level kernel)       */
+  int32_t level_staged;         /* out: 1 = the level kernel stages each env's state in LDS */
 } scg_sc_config;
 
 /* Batch state. NP = n_nodes * n_products; per-env arrays follow cfg->layout (shapes below
