@@ -32,34 +32,38 @@ __host__ __device__ __forceinline__ Num pyint(double v) { return Num{v, NK_INT};
 __host__ __device__ __forceinline__ Num f64(double v) { return Num{v, NK_F64}; }
 
 // Result kind of a binary arithmetic op (NEP 50: Python scalars adopt the other side's
-// dtype kind when it is a NumPy scalar; int64 with any float is float64).
+// dtype kind when it is a NumPy scalar; int64 with any float is float64). Written as
+// selects, not branches: kinds are per-lane data, and on the GPU a branch on them costs
+// exec-mask bookkeeping even when every lane agrees.
 __host__ __device__ __forceinline__ int np_promote(int a, int b) {
-  if (a == b) return a;
   const int lo = a < b ? a : b, hi = a < b ? b : a;
-  if (lo == NK_INT) return hi;                     // int with pyfloat/f32/f64/i64
-  if (lo == NK_PYF) return hi == NK_I64 ? NK_F64 : hi;
-  return NK_F64;                                   // f32 with f64/i64, f64 with i64
+  const int pyf = hi == NK_I64 ? NK_F64 : hi;
+  const int r = lo == NK_INT ? hi : (lo == NK_PYF ? pyf : NK_F64);
+  return a == b ? a : r;
 }
 
 // float32 rounding of an operation whose NumPy result kind is float32: operands are cast
 // to float32 (exact for float32 values, round-to-nearest for Python scalars), then the
-// operation is done in float32.
+// operation is done in float32. Both roundings are computed and the kind selects one.
 __host__ __device__ __forceinline__ Num np_add(Num a, Num b) {
   const int k = np_promote(a.k, b.k);
-  if (k == NK_F32) return Num{static_cast<double>(static_cast<float>(a.v) + static_cast<float>(b.v)), k};
-  return Num{a.v + b.v, k};
+  const double r32 = static_cast<double>(static_cast<float>(a.v) + static_cast<float>(b.v));
+  const double r64 = a.v + b.v;
+  return Num{k == NK_F32 ? r32 : r64, k};
 }
 
 __host__ __device__ __forceinline__ Num np_sub(Num a, Num b) {
   const int k = np_promote(a.k, b.k);
-  if (k == NK_F32) return Num{static_cast<double>(static_cast<float>(a.v) - static_cast<float>(b.v)), k};
-  return Num{a.v - b.v, k};
+  const double r32 = static_cast<double>(static_cast<float>(a.v) - static_cast<float>(b.v));
+  const double r64 = a.v - b.v;
+  return Num{k == NK_F32 ? r32 : r64, k};
 }
 
 __host__ __device__ __forceinline__ Num np_mul(Num a, Num b) {
   const int k = np_promote(a.k, b.k);
-  if (k == NK_F32) return Num{static_cast<double>(static_cast<float>(a.v) * static_cast<float>(b.v)), k};
-  return Num{a.v * b.v, k};
+  const double r32 = static_cast<double>(static_cast<float>(a.v) * static_cast<float>(b.v));
+  const double r64 = a.v * b.v;
+  return Num{k == NK_F32 ? r32 : r64, k};
 }
 
 // True division: int/int -> Python float, int64/int -> float64.
@@ -80,13 +84,13 @@ __host__ __device__ __forceinline__ bool np_f32_cmp(const Num& a, const Num& b) 
 }
 
 __host__ __device__ __forceinline__ bool np_lt(Num a, Num b) {
-  if (np_f32_cmp(a, b)) return static_cast<float>(a.v) < static_cast<float>(b.v);
-  return a.v < b.v;
+  const bool c32 = static_cast<float>(a.v) < static_cast<float>(b.v);
+  return np_f32_cmp(a, b) ? c32 : a.v < b.v;
 }
 
 __host__ __device__ __forceinline__ bool np_eq(Num a, Num b) {
-  if (np_f32_cmp(a, b)) return static_cast<float>(a.v) == static_cast<float>(b.v);
-  return a.v == b.v;
+  const bool c32 = static_cast<float>(a.v) == static_cast<float>(b.v);
+  return np_f32_cmp(a, b) ? c32 : a.v == b.v;
 }
 
 // Python's builtin min(a, b): b if b < a else a (keeps the chosen operand's kind).

@@ -207,9 +207,9 @@ class SupplyChainVecEnv:
     demand_table / leadtime_table: optional device int32 tensors [N, T+1, R, P] /
     [N, T, n_lt] used for every episode instead of the Philox draws (e.g. to replay the
     reference's RandomState episodes exactly).
-    kernel: "auto" (the level-parallel kernel whenever the chain has a level schedule,
-    DESIGN.md §6), "level" or "lane" (one lane walks one env's whole chain). Both give the
-    same results; the state layout follows the kernel.
+    kernel: "auto" / "lane" (one lane walks one env's whole chain) or "level" (a lane
+    group per env, one lane per node of a level). Both give the same
+    results; the state layout follows the kernel.
     """
 
     _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL}
