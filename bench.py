@@ -11,13 +11,17 @@ synthetic uniform integers in [0, 8], generated on device before timing (the pol
 output, resident in HBM). Envs shard across ranks by global id; the only collective is the
 async RCCL all-gather of per-env episode returns at each episode end.
 
-Rank 0 prints ONE JSON line. `roofline` prices the step kernel: algorithmic bytes per
-launch (DESIGN.md §6, 260 B per env on a regular week) ÷ the kernel's average duration
-from kernel-stamped HIP events (hipExtLaunchKernel start/stop) on every 8th launch of the
-timed region — 8 is coprime with the 35-week cycle, so every week kind is sampled, and the
-bytes are summed over exactly the sampled launches. Stamping every launch would add host
-time per step to the loop whose wall clock is `value`. `cpu_baseline` times oracle.beergame.BeerGameOracle — the per-env NumPy
-restatement of the reference step() — on the host's cores (rank 0, N = 1 only).
+Rank 0 prints ONE JSON line. `value` is the wall clock of the timed step loop, in which no
+launch is stamped. `roofline` prices the step kernel: algorithmic bytes per launch
+(DESIGN.md §6, 260 B per env on a regular week) ÷ the kernel's average duration, taken
+after the timed region from `--kernel-samples` more launches (whole 35-week cycles), each
+stamped by hipExtLaunchKernel with its own dispatch begin/end (the interval rocprofv3
+reports) and run alone — a stamped launch queued behind another also counts the tail of
+its predecessor, and a stamped launch is slower than a plain one, so the timed loop stays
+unstamped. `gpu_timeline_us_per_launch` is the timed region's GPU time per step (events
+on the launch stream around the loop: kernels plus the boundaries between them).
+`cpu_baseline` times oracle.beergame.BeerGameOracle — the per-env NumPy restatement of the
+reference step() — on the host's cores (rank 0, N = 1 only).
 """
 import argparse
 import json
@@ -26,7 +30,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(REPO, "gym-supplychain_amd"))
+sys.path.insert(0, os.environ.get("SCG_PKG_ROOT") or os.path.join(REPO, "gym-supplychain_amd"))
 sys.path.insert(0, REPO)
 
 N_ENVS = 65536
@@ -134,9 +138,8 @@ def main():
     ap.add_argument("--envs", type=int, default=N_ENVS, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=1.5)
-    ap.add_argument("--event-every", type=int, default=8,
-                    help="stamp every k-th timed launch with kernel events (k coprime with the 35-week "
-                         "cycle so every week kind is sampled; stamping costs host time per launch)")
+    ap.add_argument("--kernel-samples", type=int, default=350,
+                    help="launches timed one at a time with kernel-stamped events after the timed region")
     args = ap.parse_args()
 
     import torch
@@ -170,48 +173,54 @@ def main():
 
     week_actions = list(actions.unbind(0))  # the policy output of each week, resident in HBM
 
-    def run(k, events=None, every=1):
+    def run(k, events=None, isolated=False):
         for i in range(k):
-            ev = events[i // every] if events is not None and i % every == 0 else None
-            _, _, done, info = env.step(week_actions[env.week], ev)
+            _, _, done, info = env.step(week_actions[env.week], None if events is None else events[i])
             if info:
                 gather.on_episode_end(info["episode_return"])
+            if isolated:
+                torch.cuda.synchronize(device)
+
+    def week_bytes(w):
+        return N * step_bytes_per_env(plan[w], w, WEEKS, LEVELS, 2, True, True, True, True)
 
     run(args.warmup)
-    # byte accounting for the weeks the timed region will cover (lock-step, known on host)
     plan = list(env._plan)
-    w0 = env.week
-    every = max(1, args.event_every)
-    total_bytes = sampled_bytes = 0
-    for i in range(args.steps):
-        w = (w0 + i) % WEEKS + 1
-        b = N * step_bytes_per_env(plan[w], w, WEEKS, LEVELS, 2, True, True, True, True)
-        total_bytes += b
-        sampled_bytes += b if i % every == 0 else 0
-    # (start, stop) events stamped by hipExtLaunchKernel with the step kernel's own dispatch
-    # begin/end — the interval rocprofv3 reports as the kernel duration — on every
-    # `every`-th launch of the timed region
-    n_sampled = (args.steps + every - 1) // every
-    events = [(nat.hip_event(), nat.hip_event()) for _ in range(n_sampled)]
+    # timed region: plain launches, nothing stamped; GPU-timeline events on the launch stream
+    # (torch's current stream, which VecEnv.step launches on) bracket it
+    t_ev0, t_ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.steps, events, every)
+    t_ev0.record(stream)
+    run(args.steps)
+    t_ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gather.result()
     torch.cuda.synchronize()
+    timeline_ms = t_ev0.elapsed_time(t_ev1)
+    # kernel duration: a further `--kernel-samples` launches (a multiple of the 35-week cycle,
+    # so every week kind is weighted as in the timed region), each stamped with its own
+    # dispatch begin/end by hipExtLaunchKernel (the interval rocprofv3 reports) and run
+    # alone: a stamped launch queued behind another would also count its predecessor's tail
+    k_samples = max(WEEKS, args.kernel_samples // WEEKS * WEEKS)
+    w0 = env.week
+    sampled_bytes = sum(week_bytes((w0 + i) % WEEKS + 1) for i in range(k_samples))
+    events = [(nat.hip_event(), nat.hip_event()) for _ in range(k_samples)]
+    run(k_samples, events, isolated=True)
     kern_ms = sum(nat.hip_event_elapsed_ms(s, e) for s, e in events)
     for s, e in events:
         nat.hip_event_destroy(s)
         nat.hip_event_destroy(e)
+    n_sampled = k_samples
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kern_ms, timeline_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, timeline_ms = float(t[0]), float(t[1]), float(t[2])
 
     if rank == 0:
         value = N * world * args.steps / elapsed
@@ -238,7 +247,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "scg::bg_step_kernel<4>", "avg_kernel_us": avg_kernel_s * 1e6,
-                         "bytes_per_launch": total_bytes / args.steps, "launches_timed": n_sampled},
+                         "bytes_per_launch": sampled_bytes / n_sampled, "launches_timed": n_sampled,
+                         "gpu_timeline_us_per_launch": timeline_ms * 1e3 / args.steps},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)

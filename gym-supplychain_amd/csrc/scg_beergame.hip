@@ -117,25 +117,32 @@ __device__ __forceinline__ void fill_row(int32_t* __restrict__ p, int32_t x) {
   store_row<L>(p, v);
 }
 
+// Inverse CDF on uint32 thresholds: #{k : thr[k] <= u}. The table index is wave-uniform,
+// so it streams through scalar loads; no divergent search.
+__device__ __forceinline__ int32_t poisson_invert(const BgArgs& a, uint32_t u) {
+  const uint32_t* __restrict__ thr = a.pthr;
+  int32_t x = 0;
+  for (int k = 0; k < a.pthr_len; ++k) x += (thr[k] <= u) ? 1 : 0;
+  return x;
+}
+
 // Customer demand of env n for `week` (1-based): beergame_env.py:79 reads
 // customer_demand[week-1]; here per env from a table (TABLE) or drawn on device
-// (POISSON). The shared FIXED list arrives as a per-week kernel argument instead.
+// (POISSON, UNIFORM). The shared FIXED list arrives as a per-week kernel argument instead.
+// DM: the demand mode when the kernel is specialised on it, -1 to read a.demand_mode.
+template <int DM = -1>
 __device__ __forceinline__ int32_t week_demand(const BgArgs& a, int64_t n, int32_t week,
                                                uint32_t episode) {
-  if (a.demand_mode == SCG_DEMAND_TABLE) return a.demand_table[(int64_t)(week - 1) * a.n + n];
-  if (a.demand_mode == SCG_DEMAND_UNIFORM) {  // randint(lo, hi), hi exclusive (beergame2_env.py:76-77)
+  const int32_t mode = DM >= 0 ? DM : a.demand_mode;
+  if (mode == SCG_DEMAND_TABLE) return a.demand_table[(int64_t)(week - 1) * a.n + n];
+  if (mode == SCG_DEMAND_UNIFORM) {  // randint(lo, hi), hi exclusive (beergame2_env.py:76-77)
     const uint32_t w = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), episode,
                                         static_cast<uint32_t>(week - 1), SCG_STREAM_BG2_DEMAND);
     return a.demand_lo + static_cast<int32_t>((static_cast<uint64_t>(w) * static_cast<uint32_t>(a.demand_hi - a.demand_lo)) >> 32);
   }
   const uint32_t u = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n),
                                       episode, static_cast<uint32_t>(week - 1), SCG_STREAM_DEMAND);
-  // Inverse CDF on uint32 thresholds: #{k : thr[k] <= u}. The index is wave-uniform, so
-  // the table streams through scalar loads; no divergent search.
-  const uint32_t* __restrict__ thr = a.pthr;
-  int32_t x = 0;
-  for (int k = 0; k < a.pthr_len; ++k) x += (thr[k] <= u) ? 1 : 0;
-  return x;
+  return poisson_invert(a, u);
 }
 
 // reset() of one env (beergame_env.py:140-156), writing the device state rows.
@@ -232,8 +239,18 @@ __device__ __forceinline__ void zero_row(int32_t (&v)[L]) {
 
 // step(action) for one env per lane: every row this launch reads is loaded up front (one
 // round of memory latency), the week is computed in registers, then every row is stored.
-template <int L>
+template <int L, int DM>
 __global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const WeekInfo wk) {
+  // Every kernel argument the week reads, requested at once: the kernarg segment is cold
+  // in the scalar cache at every launch, and loads the compiler would otherwise sink into
+  // the branches below each cost one more dependent scalar round trip before the first
+  // row load can issue.
+  asm volatile("" ::"s"(a.n), "s"(a.inv), "s"(a.bk), "s"(a.op), "s"(a.act), "s"(a.ring), "s"(a.inv_acc),
+               "s"(a.bk_acc), "s"(a.ep_ret), "s"(a.final_ret), "s"(a.rew), "s"(a.hist), "s"(a.term_obs), "s"(a.obs),
+               "s"(a.h), "s"(a.b));
+  asm volatile("" ::"s"(wk.week), "s"(wk.read_slot), "s"(wk.write_slot), "s"(wk.mode), "s"(wk.flags),
+               "s"(wk.demand_fixed), "s"(a.demand_mode), "s"(a.pthr), "s"(a.pthr_len), "s"(a.key0), "s"(a.key1),
+               "s"(a.episode), "s"(a.env_offset), "s"(a.demand_table), "s"(a.demand_lo), "s"(a.demand_hi));
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (n >= a.n) return;
   const int64_t row = n * L;
@@ -255,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const W
   if (!autoreset && a.inv_acc) load_row<L>(a.inv_acc + row, iacc);
   if (!autoreset && a.bk_acc) load_row<L>(a.bk_acc + row, bacc);
   const int64_t ret0 = a.ep_ret ? a.ep_ret[n] : 0;
-  const int32_t demand = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, a.episode);
+  const int32_t demand = DM == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand<DM>(a, n, wk.week, a.episode);
 
   int32_t ship[L], obs[L], ic[L], bc[L];
   const int32_t reward = step_core<L>(a.h, a.b, demand, wk.mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
@@ -580,17 +597,28 @@ int launch_step2(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInf
   return check_launch("bg2_step_kernel");
 }
 
-int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk, hipEvent_t ev0,
-                hipEvent_t ev1) {
-  // hipExtLaunchKernelGGL ties the optional events to this dispatch's own start/end
-  // timestamps (the numbers rocprofv3 reports), not to separate event packets.
+template <int DM>
+int launch_step_dm(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk, hipEvent_t ev0,
+                   hipEvent_t ev1) {
   switch (L) {
-#define X(l) case l: hipExtLaunchKernelGGL(bg_step_kernel<l>, grid, dim3(kBlock), 0, s, ev0, ev1, 0, a, wk); break;
+#define X(l) case l: hipExtLaunchKernelGGL(HIP_KERNEL_NAME(bg_step_kernel<l, DM>), grid, dim3(kBlock), 0, s, ev0, ev1, 0, a, wk); break;
     SCG_LEVEL_CASES(X)
 #undef X
     default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
   }
   return check_launch("bg_step_kernel");
+}
+
+int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk, hipEvent_t ev0,
+                hipEvent_t ev1) {
+  // hipExtLaunchKernelGGL ties the optional events to this dispatch's own start/end
+  // timestamps (the numbers rocprofv3 reports), not to separate event packets.
+  switch (a.demand_mode) {
+    case SCG_DEMAND_FIXED: return launch_step_dm<SCG_DEMAND_FIXED>(L, grid, s, a, wk, ev0, ev1);
+    case SCG_DEMAND_TABLE: return launch_step_dm<SCG_DEMAND_TABLE>(L, grid, s, a, wk, ev0, ev1);
+    case SCG_DEMAND_UNIFORM: return launch_step_dm<SCG_DEMAND_UNIFORM>(L, grid, s, a, wk, ev0, ev1);
+    default: return launch_step_dm<SCG_DEMAND_POISSON>(L, grid, s, a, wk, ev0, ev1);
+  }
 }
 
 int launch_rollout(int L, dim3 grid, hipStream_t s, const BgArgs& a, int32_t K, const RolloutWeeks& weeks,

@@ -111,35 +111,27 @@ __global__ __launch_bounds__(kScBlock) void sc_step_kernel(const ScArgs a) {
   if (e.overflow) atomicOr(a.err, 1);
 }
 
-// The same step with this block's 64 envs staged in LDS — heaps, sizes, stock and action
-// rows: heap pushes/pops/walks and the stock read-modify-writes are chains of dependent
-// accesses, so they run at LDS latency instead of L2/HBM latency, and the step itself
-// issues no global load. Layout [slot][lane] (lane fastest): any mix of per-lane heap
-// positions is bank-conflict free. Rows are staged in and out with coalesced 64-lane
-// transfers, copying only the live entries (< heap size) of each lane.
+// The same step with this block's 64 env heaps staged in LDS: heap pushes/pops/walks are
+// chains of dependent accesses, so they run at LDS latency instead of L2/HBM latency.
+// Layout [slot][lane] (lane fastest): any mix of per-lane heap positions is bank-conflict
+// free. Stock stays in HBM (a few accesses per node). Rows are staged in and out with
+// coalesced 64-lane transfers, copying only the live entries (< heap size) of each lane.
 template <int MAXD>
 __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kScBlock;
-  const int64_t n = n0 + lane;
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + lane;
   const ScCtx& c = a.c;
   const int NP = c.n_nodes * c.P;
   const int slots = NP * c.H;
   double* lval = reinterpret_cast<double*>(smem);
-  double* lstock = lval + static_cast<int64_t>(slots) * kScBlock;
-  float* lact = reinterpret_cast<float*>(lstock + static_cast<int64_t>(NP) * kScBlock);
-  int32_t* ltk = reinterpret_cast<int32_t*>(lact + static_cast<int64_t>(c.A) * kScBlock);
+  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
   int32_t* lsize = ltk + static_cast<int64_t>(slots) * kScBlock;
-  // the block's action rows are one contiguous span: stage it with coalesced loads
-  const int64_t span = (a.n - n0 < kScBlock ? a.n - n0 : kScBlock) * c.A;
-  for (int64_t q = lane; q < span; q += kScBlock) lact[q] = a.act[n0 * c.A + q];
   const bool live = n < a.n;
   if (live) {
     for (int hp = 0; hp < NP; ++hp) {
       const int32_t sz = a.size[hp * a.n + n];
       lsize[hp * kScBlock + lane] = sz;
-      lstock[hp * kScBlock + lane] = a.stock[hp * a.n + n];
       for (int j = 0; j < sz; ++j) {
         const int64_t g = (static_cast<int64_t>(hp) * c.H + j) * a.n + n;
         ltk[(hp * c.H + j) * kScBlock + lane] = a.tk[g];
@@ -147,11 +139,10 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
       }
     }
   }
-  __syncthreads();
   if (!live) return;  // no block-wide sync below: every lane only touches its own column
-  ScEnv e{lstock + lane, ltk + lane, lval + lane, lsize + lane, kScBlock, kScBlock,
+  ScEnv e{a.stock + n, ltk + lane, lval + lane, lsize + lane, a.n, kScBlock,
           static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
-  const double reward = sc_step_env<MAXD>(c, e, lact + lane * c.A, a.t);
+  const double reward = sc_step_env<MAXD>(c, e, a.act + n * c.A, a.t);
   a.rew[n] = reward;
   const bool terminal = a.flags & 1;
   if (a.ep_ret) {
@@ -180,7 +171,6 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
   for (int hp = 0; hp < NP; ++hp) {
     const int32_t sz = lsize[hp * kScBlock + lane];
     a.size[hp * a.n + n] = sz;
-    a.stock[hp * a.n + n] = lstock[hp * kScBlock + lane];
     for (int j = 0; j < sz; ++j) {
       const int64_t g = (static_cast<int64_t>(hp) * c.H + j) * a.n + n;
       a.tk[g] = ltk[(hp * c.H + j) * kScBlock + lane];
@@ -437,9 +427,12 @@ bool sc_level_schedule(scg_sc_config* cfg, const scg_sc_node* nodes) {
   }
   return sc_level_lds_bytes(cfg) <= kScLdsMax;
 }
-size_t sc_lds_bytes(const scg_sc_config* cfg) {  // heaps + sizes + stock + actions
+// Heaps and sizes only: staging stock and action rows as well (+12 B per heap, +4 B per
+// action) costs sc-2perstage-v0 a block per CU (3 instead of 4 at 65,536 envs), which
+// measured 127 us against 70 us per step on MI355X (profiles/r01f_sc_variants.log).
+size_t sc_lds_bytes(const scg_sc_config* cfg) {
   const size_t NP = static_cast<size_t>(cfg->n_nodes) * cfg->n_products;
-  return kScBlock * (NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4 + 8) + static_cast<size_t>(cfg->n_actions) * 4);
+  return kScBlock * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
 }
 
 }  // namespace

@@ -20,7 +20,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(REPO, "gym-supplychain_amd"))
+sys.path.insert(0, os.environ.get("SCG_PKG_ROOT") or os.path.join(REPO, "gym-supplychain_amd"))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0
@@ -36,7 +36,7 @@ def _cpu_worker(arg):
     name, idx, budget = arg
     import numpy as np
     sys.path.insert(0, REPO)
-    sys.path.insert(0, os.path.join(REPO, "gym-supplychain_amd"))
+    sys.path.insert(0, os.environ.get("SCG_PKG_ROOT") or os.path.join(REPO, "gym-supplychain_amd"))
     from gym_supplychain_amd.envs.scenarios import SCENARIOS as BUILDERS  # config only, no GPU use
     from oracle.sc_draws import sc_demand_table
     from oracle.supplychain import SupplyChainOracle

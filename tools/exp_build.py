@@ -1,0 +1,78 @@
+"""Build experiment variants of libscgpu.so side by side (for A/B timing on the GPU box).
+
+    python tools/exp_build.py NAME [--rev GIT_REV] [--file csrc/X.h=REV ...] [-D MACRO=V ...]
+
+Writes exp/NAME/gym_supplychain_amd/ — a copy of the package whose libscgpu.so is built
+from the working-tree csrc/ (or from GIT_REV, or per-file revisions) with extra -D flags.
+Run a tool against it with SCG_PKG_ROOT=exp/NAME (bench.py and tools/bench_sc.py,
+tools/bg_variants.py honour it). exp/ is git-ignored scratch.
+"""
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "gym-supplychain_amd")
+sys.path.insert(0, PKG)
+import build_native  # noqa: E402
+
+
+def git_show(rev, path):
+    return subprocess.run(["git", "-C", REPO, "show", f"{rev}:{path}"], check=True, capture_output=True,
+                          text=True).stdout
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name")
+    ap.add_argument("--rev", default=None, help="take every csrc file and include/scgpu.h from this revision")
+    ap.add_argument("--file", action="append", default=[], help="csrc/FILE=REV: one file from a revision")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    root = os.path.join(REPO, "exp", a.name)
+    shutil.rmtree(root, ignore_errors=True)
+    csrc = os.path.join(root, "csrc")
+    inc = os.path.join(root, "include")
+    os.makedirs(csrc)
+    os.makedirs(inc)
+    for f in os.listdir(os.path.join(PKG, "csrc")):
+        src = os.path.join(PKG, "csrc", f)
+        text = git_show(a.rev, f"gym-supplychain_amd/csrc/{f}") if a.rev else open(src).read()
+        open(os.path.join(csrc, f), "w").write(text)
+    hdr = git_show(a.rev, "include/scgpu.h") if a.rev else open(os.path.join(REPO, "include", "scgpu.h")).read()
+    open(os.path.join(inc, "scgpu.h"), "w").write(hdr)
+    for spec in a.file:
+        path, rev = spec.split("=")
+        open(os.path.join(csrc, os.path.basename(path)), "w").write(git_show(rev, f"gym-supplychain_amd/{path}"))
+    pkg = os.path.join(root, "gym_supplychain_amd")
+    if a.rev:  # the Python package of that revision too (it must match the library's ABI)
+        files = subprocess.run(["git", "-C", REPO, "ls-tree", "-r", "--name-only", a.rev,
+                                "gym-supplychain_amd/gym_supplychain_amd"], check=True, capture_output=True,
+                               text=True).stdout.split()
+        for f in files:
+            dst = os.path.join(pkg, os.path.relpath(f, "gym-supplychain_amd/gym_supplychain_amd"))
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            open(dst, "w").write(git_show(a.rev, f))
+    else:
+        shutil.copytree(os.path.join(PKG, "gym_supplychain_amd"), pkg,
+                        ignore=shutil.ignore_patterns("*.so", "__pycache__"))
+    out = os.path.join(pkg, "libscgpu.so")
+    srcs = [os.path.join(csrc, s) for s in build_native.SOURCES]
+    cmd = [build_native.hipcc(), f"--offload-arch={build_native.ARCH}", "-std=c++17", "-fPIC", "-shared",
+           "-fvisibility=hidden", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall",
+           "-Wno-unused-function", "-I", inc, "-I", csrc, "-O3", "-o", out] + \
+        [f"-D{d}" for d in a.defines] + srcs
+    print("[exp_build]", " ".join(cmd))
+    subprocess.run(cmd, check=True)
+    import sysconfig
+    bout = os.path.join(pkg, "_scgpu_fast" + sysconfig.get_config_var("EXT_SUFFIX"))
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", sysconfig.get_paths()["include"], "-I", inc,
+                    os.path.join(csrc, "scg_pybind.c"), "-L", pkg, "-lscgpu", "-Wl,-rpath,$ORIGIN", "-o", bout],
+                   check=True)
+    print(f"[exp_build] {root}")
+
+
+if __name__ == "__main__":
+    main()
