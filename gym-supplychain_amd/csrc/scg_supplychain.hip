@@ -35,6 +35,10 @@ struct ScArgs {
   double* ep_ret;
   double* final_ret;
   int32_t* err;
+  double* led_v;     // build_info ledgers [2*8*P][N] (lane kernels) or null
+  int32_t* led_k;
+  double* led_fv;    // terminal-step ledger on auto-reset
+  int32_t* led_fk;
   int64_t n;
   int64_t env_offset;
   uint32_t episode;
@@ -62,7 +66,22 @@ __device__ __forceinline__ ScEnv env_view(const ScArgs& a, int64_t n, uint32_t e
     return ScEnv{a.stock + n * NP, a.tk + n * NP * a.c.H, a.val + n * NP * a.c.H, a.size + n * NP, 1, 1,
                  static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
   }
-  return ScEnv{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, a.n, static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
+  ScEnv e{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, a.n, static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
+  if (a.led_v) {
+    e.led_v = a.led_v + n;
+    e.led_k = a.led_k + n;
+    e.led_stride = a.n;
+  }
+  return e;
+}
+
+// Auto-reset keeps the finished episode's ledger (the info of the terminal step, :744-746).
+__device__ __forceinline__ void snapshot_ledger(const ScArgs& a, const ScCtx& c, int64_t n) {
+  if (!a.led_v || !a.led_fv) return;
+  for (int q = 0; q < 2 * SCG_SC_LEDGER_KEYS * c.P; ++q) {
+    a.led_fv[q * a.n + n] = a.led_v[q * a.n + n];
+    a.led_fk[q * a.n + n] = a.led_k[q * a.n + n];
+  }
 }
 
 __global__ __launch_bounds__(kScBlock) void sc_reset_kernel(const ScArgs a) {
@@ -96,6 +115,7 @@ __global__ __launch_bounds__(kScBlock) void sc_step_kernel(const ScArgs a) {
       ObsRow tout{a.term_obs, n * a.c.O, a.obs_f64};
       sc_observe(a.c, e, a.t, tout);
     }
+    snapshot_ledger(a, a.c, n);
     e.episode = a.episode + 1;
     sc_reset_env(a.c, e);
     ObsRow out{a.obs, n * a.c.O, a.obs_f64};
@@ -142,6 +162,11 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
   if (!live) return;  // no block-wide sync below: every lane only touches its own column
   ScEnv e{a.stock + n, ltk + lane, lval + lane, lsize + lane, a.n, kScBlock,
           static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
+  if (a.led_v) {
+    e.led_v = a.led_v + n;
+    e.led_k = a.led_k + n;
+    e.led_stride = a.n;
+  }
   const double reward = sc_step_env<MAXD>(c, e, a.act + n * c.A, a.t);
   a.rew[n] = reward;
   const bool terminal = a.flags & 1;
@@ -155,6 +180,7 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
       ObsRow tout{a.term_obs, n * c.O, a.obs_f64};
       sc_observe(c, e, a.t, tout);
     }
+    snapshot_ledger(a, c, n);
     e.episode = a.episode + 1;
     sc_reset_env(c, e);
     ObsRow out{a.obs, n * c.O, a.obs_f64};
@@ -323,6 +349,10 @@ int sc_check(const scg_sc_config* cfg, const scg_sc_state* st) {
     return fail(SCG_ERR_INVALID, "global env ids must fit in 32 bits");
   if (!st->stock || !st->heap_tk || !st->heap_val || !st->heap_size || !st->error_flags)
     return fail(SCG_ERR_INVALID, "state buffers stock/heap_tk/heap_val/heap_size/error_flags are required");
+  if (!st->ledger != !st->ledger_kind || !st->final_ledger != !st->final_ledger_kind)
+    return fail(SCG_ERR_INVALID, "ledger values and kinds come in pairs");
+  if (st->ledger && cfg->kernel == SCG_SC_KERNEL_LEVEL)
+    return fail(SCG_ERR_INVALID, "build_info ledgers need the lane kernel");
   return SCG_OK;
 }
 
@@ -361,6 +391,10 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   a.ep_ret = st->episode_return;
   a.final_ret = st->final_return;
   a.err = st->error_flags;
+  a.led_v = st->ledger;
+  a.led_k = st->ledger_kind;
+  a.led_fv = st->final_ledger;
+  a.led_fk = st->final_ledger_kind;
   a.n = st->n_envs;
   a.env_offset = st->env_offset;
   a.episode = st->episode;

@@ -47,7 +47,42 @@ struct ScEnv {
   int64_t local;     // index in this shard (caller tables)
   uint32_t episode;
   int32_t overflow;  // set when a push met a full heap (the push is dropped)
+  // build_info ledgers (info['sc_episode']), entry q at [q * led_stride]; null when off
+  double* led_v = nullptr;
+  int32_t* led_k = nullptr;
+  int64_t led_stride = 0;
 };
+
+// info['sc_episode'] categories in the reference's dict order (:416-417)
+enum ScLedgerKey : int {
+  LK_STOCK = 0, LK_STOCK_PEN, LK_SUPPLY, LK_PROCESS, LK_PROCESS_PEN, LK_SHIP, LK_SHIP_PEN, LK_UNMET
+};
+
+// One cost/unit entry a node's act sets (est_costs/est_units[key][p], :236-394), added to
+// the episode ledger as _update_statistics does (:750-760): the reference sums the nodes'
+// entries after the step in node order, and each entry is set at most once per act, so
+// adding it where it is set gives the same sums; entries an act leaves at the Python int 0
+// change neither value nor type of a sum, so they are skipped.
+__host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int key, int p, Num cost, Num units) {
+  if (!e.led_v) return;
+  const int64_t i0 = (static_cast<int64_t>(key) * c.P + p) * e.led_stride;
+  const int64_t i1 = (static_cast<int64_t>(SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride;
+  const Num a = np_add(Num{e.led_v[i0], e.led_k[i0]}, cost);
+  const Num b = np_add(Num{e.led_v[i1], e.led_k[i1]}, units);
+  e.led_v[i0] = a.v;
+  e.led_k[i0] = a.k;
+  e.led_v[i1] = b.v;
+  e.led_k[i1] = b.k;
+}
+
+// est_episode at reset (:684-695): every entry the Python int 0
+__host__ __device__ inline void sc_reset_ledger(const ScCtx& c, ScEnv& e) {
+  if (!e.led_v) return;
+  for (int q = 0; q < 2 * SCG_SC_LEDGER_KEYS * c.P; ++q) {
+    e.led_v[q * e.led_stride] = 0.0;
+    e.led_k[q * e.led_stride] = NK_INT;
+  }
+}
 
 __host__ __device__ __forceinline__ HeapView sc_heap(const ScCtx& c, const ScEnv& e, int node, int p) {
   const int64_t hp = static_cast<int64_t>(node) * c.P + p;
@@ -137,6 +172,7 @@ __host__ __device__ inline void sc_reset_heap(const ScCtx& c, ScEnv& e, int i, i
 __host__ __device__ inline void sc_reset_env(const ScCtx& c, ScEnv& e) {
   for (int i = 0; i < c.n_nodes; ++i)
     for (int p = 0; p < c.P; ++p) sc_reset_heap(c, e, i, p);
+  sc_reset_ledger(c, e);
 }
 
 // MAXD scalars with their NumPy kinds, the kinds packed 4 bits per entry so an unrolled
@@ -241,7 +277,10 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
   for (int p = 0; p < P; ++p) {
     double& st = sc_stock(c, e, ni, p);
     if (st > static_cast<double>(nd.stock_capacity[p])) {
-      cost = np_add(cost, np_mul(pyint(c.pen_stock), np_sub(f64(st), pyint(nd.stock_capacity[p]))));
+      const Num over = np_sub(f64(st), pyint(nd.stock_capacity[p]));
+      const Num pen = np_mul(pyint(c.pen_stock), over);
+      cost = np_add(cost, pen);
+      sc_note(c, e, LK_STOCK_PEN, p, pen, over);
       st = static_cast<double>(nd.stock_capacity[p]);
     }
   }
@@ -258,6 +297,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         ++lt_i;  // the lead-time cursor moves only when something was supplied (:252-254)
       }
       cost = np_add(cost, cst);
+      sc_note(c, e, LK_SUPPLY, p, cst, amount);
     }
   }
   if (!nd.last_level) {
@@ -286,7 +326,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         // stock update between them (:332) touches none of them. So they run fused, one
         // destination at a time, every accumulator seeing the reference's order, and no
         // per-destination array besides the split's output stays live.
-        Num leaving = pyint(0), ship_cost = pyint(0);
+        Num leaving = pyint(0), ship_cost = pyint(0), ship_units = pyint(0);
         for (int i = 0; i < D; ++i) {  // rolled: the body holds a heap push
           Num o = out.get_dyn(i);
           Num snt = o;  // amounts_to_ship = amounts.copy() (:292)
@@ -311,14 +351,24 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
           if (np_lt(pyint(0), snt))
             push.ship(c, e, ni, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
           ship_cost = np_add(ship_cost, np_mul(snt, pyint(nd.dest_costs[p][i])));
+          ship_units = np_add(ship_units, snt);  // sum(amounts_to_ship) (:356)
         }
         double& st = sc_stock(c, e, ni, p);
         st = st - leaving.v;  // float64 array element minus the promoted scalar (:332)
-        if (factory) cost = np_add(cost, np_mul(leaving, pyint(nd.processing_cost[p])));
+        if (factory) {
+          const Num proc = np_mul(leaving, pyint(nd.processing_cost[p]));
+          cost = np_add(cost, proc);
+          sc_note(c, e, LK_PROCESS, p, proc, leaving);
+        }
         cost = np_add(cost, ship_cost);
+        sc_note(c, e, LK_SHIP, p, ship_cost, ship_units);
       }
-      cost = np_add(cost, np_mul(pyint(c.pen_proc), over_proc));  // :361
-      cost = np_add(cost, np_mul(pyint(c.pen_ship), over_ship));  // :366
+      const Num pen_proc = np_mul(pyint(c.pen_proc), over_proc);  // :361
+      cost = np_add(cost, pen_proc);
+      sc_note(c, e, LK_PROCESS_PEN, p, pen_proc, over_proc);
+      const Num pen_ship = np_mul(pyint(c.pen_ship), over_ship);  // :366
+      cost = np_add(cost, pen_ship);
+      sc_note(c, e, LK_SHIP_PEN, p, pen_ship, over_ship);
       a_i += D;
     }
   } else {
@@ -328,11 +378,18 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
       double& st = sc_stock(c, e, ni, p);
       const Num served = py_min(f64(st), dem);
       st = st - served.v;
-      cost = np_add(cost, np_mul(pyint(c.pen_unmet), np_sub(dem, served)));
+      const Num unmet = np_sub(dem, served);
+      const Num pen = np_mul(pyint(c.pen_unmet), unmet);
+      cost = np_add(cost, pen);
+      sc_note(c, e, LK_UNMET, p, pen, unmet);
     }
   }
-  for (int p = 0; p < P; ++p)  // holding (:390-394)
-    cost = np_add(cost, np_mul(f64(sc_stock(c, e, ni, p)), pyint(nd.stock_cost[p])));
+  for (int p = 0; p < P; ++p) {  // holding (:390-394)
+    const Num held = f64(sc_stock(c, e, ni, p));
+    const Num hold = np_mul(held, pyint(nd.stock_cost[p]));
+    cost = np_add(cost, hold);
+    sc_note(c, e, LK_STOCK, p, hold, held);
+  }
   return cost;
 }
 

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (loads the HIP runtime libscgpu.so binds to)
 
 LIB_NAME = "libscgpu.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 SCG_OK = 0
 SCG_ERR_INVALID = 1
@@ -101,6 +101,8 @@ SC_MAX_DESTS = 32
 SC_MAX_INIT = 16
 SC_MAX_NODES = 256
 SC_MAX_LEVELS = 16
+SC_LEDGER_KEYS = 8  # info["sc_episode"] categories (supplychain_env.py:416-417)
+SC_LEDGER_NAMES = ("stock", "stock_pen", "supply", "process", "process_pen", "ship", "ship_pen", "unmet_dem")
 SC_KERNEL_AUTO, SC_KERNEL_LANE, SC_KERNEL_LEVEL = 0, 1, 2
 SC_LAYOUT_ENV_FASTEST, SC_LAYOUT_ENV_MAJOR = 0, 1
 SCG_STREAM_SC_DEMAND = 2
@@ -144,7 +146,8 @@ class ScState(ctypes.Structure):
     _fields_ = [("n_envs", ctypes.c_int64), ("env_offset", ctypes.c_int64), ("seed", ctypes.c_uint64),
                 ("episode", ctypes.c_uint32), ("time_step", ctypes.c_int32)] + [
         (f, ctypes.c_void_p) for f in ("stock", "heap_tk", "heap_val", "heap_size", "episode_return",
-                                       "final_return", "error_flags")]
+                                       "final_return", "error_flags", "ledger", "ledger_kind", "final_ledger",
+                                       "final_ledger_kind")]
 
 
 # Every symbol include/scgpu.h declares, with its ctypes signature.

@@ -15,8 +15,10 @@ Differences from the reference:
     instead of MT19937 RandomState, keyed by `seed` and the global env id;
   * actions are float32 (the declared Box dtype); the vec env's observations are float32
     by default (float64, the reference's dtype, on request and in the single-env class);
-  * normal / sinusoidal demand, demand_config_by_product and build_info are not yet
-    supported and raise NotImplementedError.
+  * normal / sinusoidal demand and demand_config_by_product are not yet supported and
+    raise NotImplementedError;
+  * build_info=True keeps info['sc_episode'] on the device (lane kernel); the drop-in env
+    returns it with the reference's per-entry NumPy types.
 """
 import ctypes
 import os
@@ -54,6 +56,10 @@ def _int(name, v):
     return v
 
 
+# NumPy type codes of ledger entries (scg_npscalar.h NpKind) -> the reference's scalar types
+_SC_TYPES = {0: lambda x: int(x), 1: float, 2: np.float32, 3: np.float64, 4: np.int64}
+
+
 class SupplyChainSpec:
     """SupplyChainEnv.__init__ (:482-628) resolved into scg_sc_node records."""
 
@@ -66,8 +72,7 @@ class SupplyChainSpec:
             raise NotImplementedError("demand_config_by_product=True is not supported on the GPU path yet")
         if demand_std is not None or demand_sen_peaks is not None:
             raise NotImplementedError("only uniform demand (demand_std=None, demand_sen_peaks=None) is supported yet")
-        if build_info:
-            raise NotImplementedError("build_info ledgers are not supported on the GPU path yet")
+        self.build_info = bool(build_info)
         P = _int("num_products", num_products)
         if not 1 <= P <= _MAXP:
             raise ValueError(f"num_products={P} outside 1..{_MAXP}")
@@ -210,6 +215,11 @@ class SupplyChainVecEnv:
     kernel: "auto" / "lane" (one lane walks one env's whole chain) or "level" (a lane
     group per env, one lane per node of a level). Both give the same
     results; the state layout follows the kernel.
+    spec.build_info: every step's info holds 'sc_episode' = {'rewards': [N], 'costs':
+    {key: [N, P]}, 'units': {key: [N, P]}} (device views, float64; the NumPy type of every
+    entry in ledger_kinds()), the reference's episode ledgers (:684-695, :750-760); with
+    auto-reset the terminal step adds 'terminal_sc_episode' for the finished episode.
+    Lane kernel only.
     """
 
     _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL}
@@ -253,6 +263,8 @@ class SupplyChainVecEnv:
         if kernel not in self._KERNELS:
             raise ValueError(f"kernel must be one of {sorted(self._KERNELS)}, got {kernel!r}")
         c.kernel = self._KERNELS[kernel]
+        if spec.build_info and c.kernel == nat.SC_KERNEL_LEVEL:
+            raise ValueError("build_info ledgers are kept by the lane kernel (kernel='lane' or 'auto')")
         nat.check(nat.lib.scg_sc_prepare(ctypes.byref(c), host_nodes))
         self.kernel = "level" if c.kernel == nat.SC_KERNEL_LEVEL else "lane"
         self._env_major = c.layout == nat.SC_LAYOUT_ENV_MAJOR
@@ -309,6 +321,18 @@ class SupplyChainVecEnv:
         s.heap_size, s.error_flags = self._heap_size.data_ptr(), self._err.data_ptr()
         s.episode_return = self._ret.data_ptr() if track_returns else None
         s.final_return = self._final_ret.data_ptr() if track_returns else None
+        self.build_info = spec.build_info
+        if self.build_info:  # [part][key][P][N], env fastest (include/scgpu.h)
+            shape = (2, nat.SC_LEDGER_KEYS, P, n_envs)
+            self._led = torch.zeros(shape, dtype=torch.float64, device=dev)
+            self._led_k = torch.zeros(shape, dtype=torch.int32, device=dev)
+            s.ledger, s.ledger_kind = self._led.data_ptr(), self._led_k.data_ptr()
+            if self.auto_reset:
+                self._fled = torch.zeros(shape, dtype=torch.float64, device=dev)
+                self._fled_k = torch.zeros(shape, dtype=torch.int32, device=dev)
+                s.final_ledger, s.final_ledger_kind = self._fled.data_ptr(), self._fled_k.data_ptr()
+            if not track_returns:
+                raise ValueError("build_info needs track_returns (sc_episode['rewards'])")
         self._st = s
         self._cfg_ref, self._st_ref = ctypes.byref(self._cfg), ctypes.byref(self._st)
         self._done_flag = ctypes.c_int32(0)
@@ -359,8 +383,39 @@ class SupplyChainVecEnv:
             info = {"terminal_observation": self._term_obs}
             if self._final_ret is not None:
                 info["episode_return"] = self._final_ret
+            if self.build_info:
+                info["sc_episode"] = self._ledger_views(self._led, self._ret if self.auto_reset else self._final_ret)
+                if self.auto_reset:
+                    info["terminal_sc_episode"] = self._ledger_views(self._fled, self._final_ret)
             return self._obs, self._rew, self._done_true, info
+        if self.build_info:
+            return self._obs, self._rew, self._done_false, {"sc_episode": self._ledger_views(self._led, self._ret)}
         return self._obs, self._rew, self._done_false, {}
+
+    def _ledger_views(self, led, rewards):
+        P, names = self.spec.P, nat.SC_LEDGER_NAMES
+        return {"rewards": rewards,
+                "costs": {k: led[0, j].permute(1, 0) for j, k in enumerate(names)},
+                "units": {k: led[1, j].permute(1, 0) for j, k in enumerate(names)}}
+
+    def ledger_kinds(self, final=False):
+        """NumPy type codes [2, 8, P, N] of the ledger entries (0 int, 1 float, 2 float32,
+        3 float64, 4 int64)."""
+        return self._fled_k if final else self._led_k
+
+    def sc_episode(self, env, final=False):
+        """info['sc_episode'] of one env as the reference builds it (:684-695): Python /
+        NumPy scalars of the reference's types, lists per product."""
+        if not self.build_info:
+            raise ValueError("the env was built with build_info=False")
+        led, kinds, ret = (self._fled, self._fled_k, self._final_ret) if final else (self._led, self._led_k, self._ret)
+        v = led[..., env].cpu().numpy()
+        k = kinds[..., env].cpu().numpy()
+        out = {"rewards": np.float64(ret[env].item())}
+        for part, name in ((0, "costs"), (1, "units")):
+            out[name] = {key: [_SC_TYPES[int(k[part, j, p])](v[part, j, p]) for p in range(self.spec.P)]
+                         for j, key in enumerate(nat.SC_LEDGER_NAMES)}
+        return out
 
     def check_errors(self):
         """Raise if any env's in-transit heap overflowed its capacity (never expected: the
@@ -435,7 +490,8 @@ class SupplyChainEnv:
     """Drop-in for gym_supplychain.envs.SupplyChainEnv (:478-813), one env on the GPU.
 
     Same constructor keywords; reset() -> float64 obs in [-1, 1]; step(action) ->
-    (obs, np.float64 reward, done, {}); seed(seed). Demand and stochastic lead times are
+    (obs, np.float64 reward, done, info); seed(seed). info is {} or, with build_info,
+    {'sc_episode': ledgers} (one dict per episode, updated in place each step). Demand and stochastic lead times are
     drawn with Philox from `seed` (see module docstring).
     """
 
@@ -472,6 +528,8 @@ class SupplyChainEnv:
         self._act_dev = torch.zeros((1, spec.n_actions), dtype=torch.float32, device=self._vec.device)
         self._obs_host = torch.zeros((1, spec.n_obs), dtype=torch.float64, pin_memory=pin)
         self._rew_host = torch.zeros(1, dtype=torch.float64, pin_memory=pin)
+        self.build_info = spec.build_info
+        self.est_episode = None
 
     @property
     def time_step(self):
@@ -484,6 +542,9 @@ class SupplyChainEnv:
         obs = self._vec.reset()
         self.current_reward = 0
         self.episode_rewards = 0
+        if self.build_info:  # a new ledger dict per episode, mutated by every step (:677-678, :796)
+            self.est_episode = self._vec.sc_episode(0)
+            self.est_episode["rewards"] = 0
         self.current_state = obs[0].cpu().numpy().copy()
         return self.current_state
 
@@ -499,7 +560,11 @@ class SupplyChainEnv:
         self.episode_rewards += self.current_reward
         if self.time_step == self.total_time_steps:
             self._vec.check_errors()
-        return self.current_state, self.current_reward, self.time_step == self.total_time_steps, {}
+        info = {}
+        if self.build_info:
+            self.est_episode.update(self._vec.sc_episode(0))
+            info = {"sc_episode": self.est_episode}
+        return self.current_state, self.current_reward, self.time_step == self.total_time_steps, info
 
     @property
     def stock(self):

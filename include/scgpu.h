@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SCG_ABI_VERSION 1
+#define SCG_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define SCG_API __attribute__((visibility("default")))
@@ -217,6 +217,7 @@ SCG_API int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, 
 #define SCG_SC_MAX_INIT 16
 #define SCG_SC_MAX_NODES 256
 #define SCG_SC_MAX_LEVELS 16
+#define SCG_SC_LEDGER_KEYS 8 /* info['sc_episode'] cost/unit categories (:416-417) */
 
 /* SupplyChain kernels (scg_sc_config.kernel) and the state layouts they use. */
 #define SCG_SC_KERNEL_AUTO 0
@@ -300,6 +301,15 @@ typedef struct scg_sc_state {
   double* episode_return;       /* [N] optional                                             */
   double* final_return;         /* [N] optional: return at the terminal step                */
   int32_t* error_flags;         /* [1] DEVICE, sticky: bit 0 = a heap exceeded capacity    */
+  /* build_info ledgers, info['sc_episode'] (:684-695, :750-760): optional, lane kernel only.
+     Entry ((part * SCG_SC_LEDGER_KEYS + key) * P + p), part 0 = costs, 1 = units, keys in
+     the reference's order (stock, stock_pen, supply, process, process_pen, ship, ship_pen,
+     unmet_dem); value in ledger, NumPy type (0 int, 1 float, 2 float32, 3 float64, 4 int64)
+     in ledger_kind. The final_* pair receives the terminal step's ledger on auto-reset. */
+  double* ledger;               /* [2 * 8 * P][N] */
+  int32_t* ledger_kind;         /* [2 * 8 * P][N] */
+  double* final_ledger;         /* [2 * 8 * P][N] optional */
+  int32_t* final_ledger_kind;   /* [2 * 8 * P][N] optional */
 } scg_sc_state;
 
 /* sizeof(scg_sc_node), sizeof(scg_sc_config), sizeof(scg_sc_state), to check FFI bindings. */

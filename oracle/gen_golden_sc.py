@@ -4,7 +4,9 @@ Runs gym_supplychain's SupplyChainEnv family (imported read-only from /root/refe
 the inert gym stand-in of oracle/refharness/) per env, with explicit float32 actions and
 with the episode's demand / lead-time tables replaced right after reset() by the tables
 the device draws (oracle/sc_draws.py), and records per step: observation, reward, node
-stocks and every in-transit heap in storage order (time, amount, amount type). The
+stocks, every in-transit heap in storage order (time, amount, amount type) and, with
+build_info switched on, the episode ledgers of info['sc_episode'] (value and type of every
+cost/unit entry). The
 scenario's nodes_info and constructor kwargs are captured from the reference's own
 factory classes and stored as JSON next to the arrays. Nothing is written under
 /root/reference; without it the script exits leaving the committed fixtures alone.
@@ -28,6 +30,8 @@ from oracle.sc_draws import sc_demand_table, sc_leadtime_table  # noqa: E402
 
 # Amount type codes in recorded heaps (amounts are float32, float64 or int)
 KIND = {int: 0, float: 1, np.float32: 2, np.float64: 3, np.int64: 4}
+# info['sc_episode'] cost/unit categories in the reference's dict order (:416-417, :685-686)
+LEDGER_KEYS = ("stock", "stock_pen", "supply", "process", "process_pen", "ship", "ship_pen", "unmet_dem")
 
 CASES = {
     # BASELINE config 3 scenario (sc-2perstage-v0 defaults), shortened horizon
@@ -127,6 +131,16 @@ def run_case(name, spec):
                actions=np.zeros((T, N, n_act), dtype=np.float32),
                demands=np.zeros((N, T + 1, R, P), dtype=np.int64),
                leadtimes=np.zeros((N, T, max(n_lt, 1)), dtype=np.int64))
+    # build_info on (the factories do not forward it): env and nodes keep the per-episode
+    # ledgers of info['sc_episode'] (:214-218, :684-695, :750-760); nothing else changes
+    env.build_info = True
+    for nd in env.nodes:
+        nd.build_info = True
+    nk = len(LEDGER_KEYS)
+    for key, dt in (("led_cost", np.float64), ("led_units", np.float64)):
+        rec[key] = np.zeros((T, N, nk, P), dtype=dt)
+        rec[key + "_k"] = np.zeros((T, N, nk, P), dtype=np.int8)
+    rec["led_rewards"] = np.zeros((T, N))
     for n in range(N):
         env.seed(n)
         env.reset()
@@ -149,6 +163,14 @@ def run_case(name, spec):
             rec["reward"][t, n] = r
             rec["stock"][t + 1, n] = [np.asarray(nd.stock, dtype=np.float64) for nd in env.nodes]
             rec["heap_t"][t + 1, n], rec["heap_v"][t + 1, n], rec["heap_k"][t + 1, n] = _heap_arrays(env, H)
+            led = info["sc_episode"]
+            rec["led_rewards"][t, n] = float(led["rewards"])
+            for j, key in enumerate(LEDGER_KEYS):
+                for p in range(P):
+                    for part, name in (("costs", "led_cost"), ("units", "led_units")):
+                        x = led[part][key][p]
+                        rec[name][t, n, j, p] = float(x)
+                        rec[name + "_k"][t, n, j, p] = KIND[type(x)]
     used = int((rec["heap_t"] >= 0).sum(axis=-1).max())
     for k in ("heap_t", "heap_v", "heap_k"):
         rec[k] = rec[k][..., :max(used, 1)]

@@ -114,10 +114,25 @@ def _split_shipment(values, limit, unit_costs):
     return amounts
 
 
-def _node_act(nd, actions, leadtimes, t, demand):
-    """SC_Node.act (:208-396). Returns the node's cost; mutates nd.stock / heaps."""
+LEDGER_KEYS = ("stock", "stock_pen", "supply", "process", "process_pen", "ship", "ship_pen", "unmet_dem")
+
+
+def _node_act(nd, actions, leadtimes, t, demand, est=None):
+    """SC_Node.act (:208-396). Returns the node's cost; mutates nd.stock / heaps. With
+    `est` = (costs, units) dicts of per-product lists (build_info, :214-218) it also records
+    the node's cost/unit entries of this step where the reference sets them."""
     P = nd.P
     cost = 0
+    if est is not None:
+        for d in est:
+            for key in LEDGER_KEYS:
+                d[key] = [0] * P
+
+    def note(key, p, c, u):
+        if est is not None:
+            est[0][key][p] = c
+            est[1][key][p] = u
+
     lt_i = 0
     received = np.zeros(P)
     for p, heap in enumerate(nd.heaps):                                   # :222-225
@@ -127,6 +142,7 @@ def _node_act(nd, actions, leadtimes, t, demand):
     for p in range(P):                                                    # :232-240
         if nd.stock[p] > nd.stock_cap[p]:
             cost += nd.pen_stock * (nd.stock[p] - nd.stock_cap[p])
+            note("stock_pen", p, nd.pen_stock * (nd.stock[p] - nd.stock_cap[p]), nd.stock[p] - nd.stock_cap[p])
             nd.stock[p] = nd.stock_cap[p]
     a_i = 0
     if nd.n_supply > 0:                                                   # :244-259
@@ -139,6 +155,7 @@ def _node_act(nd, actions, leadtimes, t, demand):
                     heapq.heappush(nd.heaps[p], (t + leadtimes[lt_i], amount))
                     lt_i += 1                       # cursor advances only on a shipment (:252-254)
                 cost += c
+                note("supply", p, c, amount)
     if not nd.last_level:                                                 # :262-375
         ship_left = nd.ship_cap.copy()
         proc_left = nd.processing_capacity
@@ -172,13 +189,18 @@ def _node_act(nd, actions, leadtimes, t, demand):
                 nd.stock[p] -= leaving
                 if nd.processing_capacity > 0:                            # :337-341
                     cost += leaving * nd.processing_cost[p]
+                    note("process", p, leaving * nd.processing_cost[p], leaving)
                 for i in range(D):                                        # :344-348
                     if sent[i] > 0:
                         heapq.heappush(nd.dests[i].heaps[p], (t + leadtimes[lt_i], sent[i]))
                     lt_i += 1
-                cost += sum(sent[i] * nd.dest_costs[p][i] for i in range(D))   # :352-353
+                ship_costs = sum(sent[i] * nd.dest_costs[p][i] for i in range(D))   # :352-353
+                cost += ship_costs
+                note("ship", p, ship_costs, sum(sent))
             cost += nd.pen_process * over_proc                            # :361
+            note("process_pen", p, nd.pen_process * over_proc, over_proc)
             cost += nd.pen_ship * over_ship                               # :366
+            note("ship_pen", p, nd.pen_ship * over_ship, over_ship)
             a_i += D
             lt_i = lt_base                       # same lead times for every product (:375)
     else:                                                                 # :379-387
@@ -186,8 +208,10 @@ def _node_act(nd, actions, leadtimes, t, demand):
             served = min(nd.stock[p], demand[p])
             nd.stock[p] -= served
             cost += nd.pen_unmet * (demand[p] - served)
+            note("unmet_dem", p, nd.pen_unmet * (demand[p] - served), demand[p] - served)
     for p in range(P):                                                    # :390-394
         cost += nd.stock[p] * nd.stock_cost[p]
+        note("stock", p, nd.stock[p] * nd.stock_cost[p], nd.stock[p])
     return cost
 
 
@@ -221,8 +245,9 @@ class SupplyChainOracle:
     def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
                  exceeded_process_capacity_cost=1000, exceeded_ship_capacity_cost=1000, demand_range=(10, 20),
                  processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2, max_leadtime=2,
-                 total_time_steps=360):
+                 total_time_steps=360, build_info=False):
         P = num_products
+        self.build_info = build_info
         pens = (exceeded_stock_capacity_cost, exceeded_process_capacity_cost, exceeded_ship_capacity_cost,
                 unmet_demand_cost)
         by_name = {}
@@ -258,6 +283,10 @@ class SupplyChainOracle:
         if self.stochastic:
             self.leadtimes = np.asarray(leadtimes, dtype=np.int64).reshape(self.T, self.n_lt)
         self.episode_rewards = 0
+        if self.build_info:                                                   # :677-678, :684-695
+            self.est_episode = {"rewards": 0, "costs": {k: [0] * self.P for k in LEDGER_KEYS},
+                                "units": {k: [0] * self.P for k in LEDGER_KEYS}}
+            self._est = ({}, {})
         return self._obs()
 
     def step(self, action):
@@ -278,10 +307,23 @@ class SupplyChainOracle:
             if nd.last_level:
                 demand = self.demands[self.t - 1, r_i]
                 r_i += 1
-            total += _node_act(nd, acts, lts, self.t, demand)
+            est = None
+            if self.build_info:
+                est = nd.est = ({}, {})
+            total += _node_act(nd, acts, lts, self.t, demand, est)
         reward = -total
         self.episode_rewards += reward
-        return self._obs(), reward, self.t == self.T, {}
+        info = {}
+        if self.build_info:                                                   # :744-746, :750-760
+            self.est_episode["rewards"] += reward
+            for part, j in (("costs", 0), ("units", 1)):
+                acc = self.est_episode[part]
+                for nd in self.nodes:
+                    for key, vals in nd.est[j].items():
+                        for p in range(self.P):
+                            acc[key][p] += vals[p]
+            info = {"sc_episode": self.est_episode}
+        return self._obs(), reward, self.t == self.T, info
 
     def _obs(self):                                                           # :762-791
         dem = (self.demands[self.t, :].flatten() - self.lo) / (self.hi - self.lo)

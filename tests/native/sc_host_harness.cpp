@@ -24,7 +24,7 @@ struct HostSched {
 static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
                         uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
                         double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
-                        int32_t* heap_size) {
+                        int32_t* heap_size, double* ledger = nullptr, int32_t* ledger_kind = nullptr) {
   scg::ScCtx c;
   std::memset(&c, 0, sizeof(c));
   c.nodes = nodes;
@@ -56,6 +56,15 @@ static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node*
   double* val = heap_val;
   int32_t* sz = heap_size;
   scg::ScEnv e{st, tk, val, sz, 1, 1, env_id, 0, episode, 0};
+  // build_info ledger: a running [2*8*P] buffer, copied out after every step
+  const int LQ = 2 * SCG_SC_LEDGER_KEYS * c.P;
+  std::vector<double> led_v(LQ);
+  std::vector<int32_t> led_k(LQ);
+  if (ledger) {
+    e.led_v = led_v.data();
+    e.led_k = led_k.data();
+    e.led_stride = 1;
+  }
   scg::sc_reset_env(c, e);
   auto sink = [&](double* row) { return [row](int o, double x) { row[o] = x; }; };
   {
@@ -72,6 +81,11 @@ static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node*
     std::memcpy(heap_size + t * NP, heap_size + (t - 1) * NP, sizeof(int32_t) * NP);
     scg::ScEnv et{stock + t * NP, heap_tk + static_cast<int64_t>(t) * NP * c.H,
                   heap_val + static_cast<int64_t>(t) * NP * c.H, heap_size + t * NP, 1, 1, env_id, 0, episode, 0};
+    if (ledger) {
+      et.led_v = led_v.data();
+      et.led_k = led_k.data();
+      et.led_stride = 1;
+    }
     const float* a = actions + static_cast<int64_t>(t - 1) * c.A;
     if (level) {  // sc_level_kernel's phases, lanes in turn
       scg::ScLevels lv;
@@ -107,6 +121,10 @@ static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node*
     }
     auto out = sink(obs + static_cast<int64_t>(t) * c.O);
     scg::sc_observe(c, et, t, out);
+    if (ledger) {
+      std::memcpy(ledger + static_cast<int64_t>(t - 1) * LQ, led_v.data(), sizeof(double) * LQ);
+      std::memcpy(ledger_kind + static_cast<int64_t>(t - 1) * LQ, led_k.data(), sizeof(int32_t) * LQ);
+    }
     if (et.overflow) return 1;
   }
   return e.overflow;
@@ -125,4 +143,12 @@ extern "C" int sch_episode_level(const scg_sc_config* cfg, const scg_sc_node* no
                                  int32_t* heap_size) {
   return episode_impl(true, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
                       heap_val, heap_size);
+}
+
+extern "C" int sch_episode_ledger(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                                  uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps,
+                                  const float* actions, double* obs, double* rewards, double* stock, int32_t* heap_tk,
+                                  double* heap_val, int32_t* heap_size, double* ledger, int32_t* ledger_kind) {
+  return episode_impl(false, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+                      heap_val, heap_size, ledger, ledger_kind);
 }

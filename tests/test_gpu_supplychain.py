@@ -20,7 +20,8 @@ def _vec(meta, n, **kw):
     ekw = dict(meta["kwargs"])
     ekw.pop("seed", None)
     kw.setdefault("seed", meta["seed"])
-    return SupplyChainVecEnv(n, meta["nodes_info"], device=DEV, **kw, **ekw)
+    ekw.update(kw)
+    return SupplyChainVecEnv(n, meta["nodes_info"], device=DEV, **ekw)
 
 
 def _check_heaps(env, g, t, n, name):
@@ -231,3 +232,99 @@ def test_level_kernel_equals_lane_kernel(scenario, kw):
             assert torch.equal(i0["episode_return"], i1["episode_return"])
     for e in envs:
         e.check_errors()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_ledgers_match_reference(name):
+    """build_info: info['sc_episode'] on the device against the reference's ledgers after
+    every step — values and NumPy types of every cost/unit entry, exactly."""
+    from gym_supplychain_amd import _native as nat
+    g = load_sc(name)
+    meta = g["meta"]
+    T, N = meta["T"], g["obs"].shape[1]
+    env = _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, build_info=True)
+    assert env.kernel == "lane"
+    env.reset()
+    acts = torch.as_tensor(g["actions"], device=DEV)
+    for t in range(T):
+        _, rew, _, info = env.step(acts[t])
+        led = info["sc_episode"]
+        for j, key in enumerate(nat.SC_LEDGER_NAMES):
+            assert np.array_equal(led["costs"][key].cpu().numpy(), g["led_cost"][t, :, j]), (name, t, key)
+            assert np.array_equal(led["units"][key].cpu().numpy(), g["led_units"][t, :, j]), (name, t, key)
+        k = env.ledger_kinds().cpu().numpy()                       # [2, 8, P, N]
+        assert np.array_equal(k[0].transpose(2, 0, 1), g["led_cost_k"][t]), (name, t)
+        assert np.array_equal(k[1].transpose(2, 0, 1), g["led_units_k"][t]), (name, t)
+        assert np.allclose(led["rewards"].cpu().numpy(), g["led_rewards"][t], rtol=1e-12, atol=0)
+    env.check_errors()
+
+
+def test_ledgers_autoreset_and_reference_known_answers():
+    """Terminal-step ledger kept across auto-reset; the reference's own ledger tests
+    (test_multiproduct.py:123-237) through the drop-in types."""
+    from gym_supplychain_amd import SupplyChainVecEnv
+    from test_oracle_supplychain import KA_LEDGERS, ka_multiproduct_chain
+    nodes, kw = ka_multiproduct_chain()
+    for case, (T, acts, want) in sorted(KA_LEDGERS.items()):
+        dem = np.random.RandomState(0).randint(0, 6, size=(1, T + 1, 1, 2))
+        env = SupplyChainVecEnv(1, nodes, device=DEV, obs_dtype=torch.float64, auto_reset=False, build_info=True,
+                                total_time_steps=T, demand_table=torch.as_tensor(dem, dtype=torch.int32, device=DEV),
+                                **kw)
+        env.reset()
+        for a in acts:
+            env.step(torch.as_tensor(2 * np.array(a, dtype=np.float32) - 1, device=DEV).reshape(1, -1))
+        got = env.sc_episode(0)
+        for key, (units, costs) in want.items():
+            assert got["units"][key] == units and got["costs"][key] == costs, (case, key)
+    # auto-reset: 2 episodes of 7 steps, oracle ledgers at every terminal step
+    from gym_supplychain_amd.envs.scenarios import two_per_stage_nodes
+    nodes, kw = two_per_stage_nodes(total_time_steps=7, build_info=True)
+    kw.pop("seed")
+    N, seed = 300, 99
+    env = SupplyChainVecEnv(N, nodes, seed=seed, device=DEV, obs_dtype=torch.float64, auto_reset=True, **kw)
+    sp = env.spec
+    okw = dict(num_products=sp.P, demand_range=sp.demand_range, processing_ratio=sp.processing_ratio,
+               total_time_steps=7, **sp.penalties)
+    env.reset()
+    gen = torch.Generator(device=DEV).manual_seed(4)
+    for ep in range(2):
+        oracles = []
+        for n in (0, 150, 299):
+            o = SupplyChainOracle(nodes, build_info=True, **okw)
+            o.reset(sc_demand_table(seed, n, ep, 7, sp.n_retailers, sp.P, *sp.demand_range))
+            oracles.append((n, o))
+        for t in range(7):
+            a = torch.rand((N, env.n_actions), generator=gen, device=DEV) * 2 - 1
+            _, _, _, info = env.step(a)
+            a_np = a.cpu().numpy()
+            for n, o in oracles:
+                _, _, _, oinfo = o.step(a_np[n].copy())
+            if t < 6:
+                assert "terminal_sc_episode" not in info
+        for n, o in oracles:
+            got = env.sc_episode(n, final=True)
+            want = o.est_episode
+            assert got["costs"] == want["costs"] and got["units"] == want["units"], (ep, n)
+            assert [type(x) for x in got["costs"]["ship"]] == [type(x) for x in want["costs"]["ship"]]
+            assert got["rewards"] == pytest.approx(float(want["rewards"]), rel=1e-12)
+        assert all(float(x) == 0 for x in env.sc_episode(0)["costs"]["stock"])   # fresh episode
+
+
+def test_drop_in_env_build_info():
+    """The drop-in class with build_info=True: info['sc_episode'] every step, one dict per
+    episode mutated in place, costs summing to -rewards (the reference's check_rewards,
+    tests/utils.py:3-12)."""
+    from gym_supplychain_amd import SupplyChain2perStageEnv
+    e = SupplyChain2perStageEnv(total_time_steps=6, seed=5, build_info=True)
+    e.reset()
+    rng = np.random.RandomState(0)
+    total, first = 0.0, None
+    for t in range(6):
+        _, r, done, info = e.step(rng.uniform(-1, 1, 14).astype(np.float32))
+        total += r
+        led = info["sc_episode"]
+        first = led if first is None else first
+        assert led is first and isinstance(led["rewards"], np.float64)
+        assert np.isclose(led["rewards"], total)
+        assert np.isclose(total, -sum(float(x) for k in led["costs"] for x in led["costs"][k]))
+    assert done

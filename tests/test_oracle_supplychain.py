@@ -109,3 +109,75 @@ def test_reference_known_answers_chain_dynamics():
         obs, r, _, _ = o.step(2 * np.array(act) - 1)
         assert np.allclose(obs, want_obs)
         assert np.round(r, 3) == want_r
+
+
+KIND = {int: 0, float: 1, np.float32: 2, np.float64: 3, np.int64: 4}
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_ledgers_match_reference(name):
+    """build_info=True: info['sc_episode'] (:684-695, :750-760) — every cost/unit entry's value
+    and NumPy type after every step, as the reference recorded them."""
+    from oracle.supplychain import LEDGER_KEYS
+    g = load_sc(name)
+    meta = g["meta"]
+    T, N = meta["T"], g["obs"].shape[1]
+    for n in range(N):
+        o = SupplyChainOracle(meta["nodes_info"], build_info=True, **g["oracle_kwargs"])
+        o.reset(g["demands"][n], g["leadtimes"][n] if meta["n_lt"] else None)
+        for t in range(T):
+            _, r, _, info = o.step(g["actions"][t, n].copy())
+            led = info["sc_episode"]
+            assert float(led["rewards"]) == g["led_rewards"][t, n]
+            for j, key in enumerate(LEDGER_KEYS):
+                for part, f in (("costs", "led_cost"), ("units", "led_units")):
+                    got = led[part][key]
+                    assert [float(x) for x in got] == g[f][t, n, j].tolist(), (name, n, t, key, part)
+                    assert [KIND[type(x)] for x in got] == g[f + "_k"][t, n, j].tolist(), (name, n, t, key, part)
+
+
+# Known answers of the reference's ledger tests (test_multiproduct.py:123-237): a 4-node
+# serial chain with 2 products, penalties 101/102/103, RandomState(0) demand in [0, 5].
+# Data only: (actions per step, then {key: (units, costs)} asserted after the last step).
+def ka_multiproduct_chain():
+    nodes = {}
+    common = dict(initial_stock=[10, 20], stock_capacity=[100, 200], stock_cost=[1, 2])
+    nodes["Supplier"] = dict(common, supply_capacity=[50, 50], supply_cost=[5, 10], destinations=["Factory"],
+                             dest_costs=[[2], [3]], ship_capacity=[100, 100])
+    nodes["Factory"] = dict(common, processing_capacity=50, processing_cost=[10, 20], destinations=["Wholesal"],
+                            dest_costs=[[2], [3]], ship_capacity=[100, 100])
+    nodes["Wholesal"] = dict(common, destinations=["Retailer"], dest_costs=[[2], [3]], ship_capacity=[100, 100])
+    nodes["Retailer"] = dict(common, last_level=True)
+    kw = dict(num_products=2, unmet_demand_cost=1000, exceeded_stock_capacity_cost=101,
+              exceeded_process_capacity_cost=102, exceeded_ship_capacity_cost=103, demand_range=(0, 5),
+              processing_ratio=2, stochastic_leadtimes=False, avg_leadtime=2, max_leadtime=2)
+    return nodes, kw
+
+
+KA_SUPPLY = [1, 1, 0, 0, 0, 0, 0, 0]
+KA_SEND_ALL = [1] * 8
+KA_SUPPLIER_FULL = [1, 1, 1, 1, 0, 0, 0, 0]
+KA_LEDGERS = {
+    "basic": (5, [KA_SUPPLY, KA_SEND_ALL, KA_SEND_ALL, KA_SEND_ALL],
+              {"stock": ([57, 122], [57, 244]), "stock_pen": ([0, 0], [0, 0]), "supply": ([200, 200], [1000, 2000]),
+               "process": ([20, 40], [200, 800]), "process_pen": ([0, 0], [0, 0]), "ship": ([135, 170], [270, 510]),
+               "ship_pen": ([0, 0], [0, 0]), "unmet_dem": ([0, 0], [0, 0])}),
+    "pen_4": (5, [KA_SUPPLY] * 4, {"stock_pen": ([10, 0], [1010, 0])}),
+    "pen_5": (5, [KA_SUPPLY] * 4 + [KA_SEND_ALL],
+              {"ship_pen": ([0, 70], [0, 103 * 70]), "unmet_dem": ([3, 0], [3000, 0])}),
+    "processpen": (6, [KA_SUPPLY] + [KA_SUPPLIER_FULL] * 4 + [KA_SEND_ALL],
+                   {"process_pen": ([50, 140], [102 * 50, 102 * 140])}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(KA_LEDGERS))
+def test_reference_known_answers_ledgers(case):
+    T, acts, want = KA_LEDGERS[case]
+    nodes, kw = ka_multiproduct_chain()
+    o = SupplyChainOracle(nodes, build_info=True, total_time_steps=T, **kw)
+    o.reset(np.random.RandomState(0).randint(0, 6, size=(T + 1, 1, 2)))   # env.seed(0) demand table
+    for a in acts:
+        _, _, _, info = o.step(2 * np.array(a) - 1)
+    for key, (units, costs) in want.items():
+        assert info["sc_episode"]["units"][key] == units, key
+        assert info["sc_episode"]["costs"][key] == costs, key

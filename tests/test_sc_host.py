@@ -69,3 +69,22 @@ def test_host_build_of_kernel_body_matches_reference(harness, name, kernel):
                 assert (tk[s, hp, :k] >> 3).tolist() == gt[s, hp, :k].tolist()
                 assert val[s, hp, :k].tolist() == gv[s, hp, :k].tolist()
         assert H >= gt.shape[-1]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_host_build_ledgers_match_reference(harness, name):
+    """build_info: the kernel body's ledger notes (sc_note) against info['sc_episode'] as the
+    reference recorded it after every step — values and NumPy types, exactly."""
+    import native_harness
+    from gym_supplychain_amd import _native as nat
+    g = load_sc(name)
+    meta = g["meta"]
+    spec, c, nodes, thr = _setup(g, nat.SC_KERNEL_LANE)
+    for n in range(g["obs"].shape[1]):
+        rc, obs, rew, _, _, (led_v, led_k) = native_harness.run_episode(harness, c, nodes, thr, meta["seed"], n, 0,
+                                                                       g["actions"][:, n], ledger=True)
+        assert rc == 0
+        assert np.array_equal(led_v[:, 0], g["led_cost"][:, n]) and np.array_equal(led_v[:, 1], g["led_units"][:, n])
+        assert np.array_equal(led_k[:, 0], g["led_cost_k"][:, n]), name
+        assert np.array_equal(led_k[:, 1], g["led_units_k"][:, n]), name
+        assert np.allclose(np.cumsum(rew), g["led_rewards"][:, n], rtol=1e-12, atol=0)
