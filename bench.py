@@ -69,7 +69,7 @@ def step_bytes_per_env(plan_word, week, T, L, ring_initial_slots, ledgers, histo
     return b
 
 
-def pmc_traffic(kernel_substr="bg_step_kernel<4>", n_envs=N_ENVS):
+def pmc_traffic(kernel_substr="bg_step_kernel<4, 2>", n_envs=N_ENVS):
     """HBM bytes per launch of the step kernel from the latest committed PMC summary
     (profiles/rNN_pmc_summary.json, written by tools/pmc_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench at 65,536 envs; FETCH_SIZE
@@ -246,7 +246,7 @@ def main():
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "scg::bg_step_kernel<4>", "avg_kernel_us": avg_kernel_s * 1e6,
+                         "kernel": "scg::bg_step_kernel<4, 2> (L = 4, Poisson demand)", "avg_kernel_us": avg_kernel_s * 1e6,
                          "bytes_per_launch": sampled_bytes / n_sampled, "launches_timed": n_sampled,
                          "gpu_timeline_us_per_launch": timeline_ms * 1e3 / args.steps},
         }

@@ -376,8 +376,7 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   c.stochastic = cfg->stochastic_leadtimes;
   c.n_lt = cfg->n_leadtimes;
   c.lt_thr_len = cfg->leadtime_poisson_len;
-  c.lo = cfg->demand_lo;
-  c.hi = cfg->demand_hi;
+  sc_ctx_demand(c, cfg);
   c.pen_unmet = cfg->unmet_demand_cost;
   c.pen_stock = cfg->exceeded_stock_capacity_cost;
   c.pen_proc = cfg->exceeded_process_capacity_cost;
@@ -493,8 +492,20 @@ int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
     return fail(SCG_ERR_INVALID, "total_time_steps=%d out of range", cfg->total_time_steps);
   if (cfg->avg_leadtime < 1 || cfg->max_leadtime < 1)
     return fail(SCG_ERR_INVALID, "lead times must be >= 1 (avg %d, max %d)", cfg->avg_leadtime, cfg->max_leadtime);
-  if (cfg->demand_hi <= cfg->demand_lo)
+  if (!cfg->demand_models && cfg->demand_hi <= cfg->demand_lo)
     return fail(SCG_ERR_INVALID, "demand_range (%d, %d) must have lo < hi", cfg->demand_lo, cfg->demand_hi);
+  for (int p = 0; cfg->demand_models && p < P; ++p) {
+    const int k = cfg->demand_kind[p];
+    if (k < SCG_SC_DEMAND_UNIFORM || k > SCG_SC_DEMAND_SINE_UNIFORM)
+      return fail(SCG_ERR_INVALID, "product %d: demand kind %d is not a SCG_SC_DEMAND_* value", p, k);
+    if (cfg->demand_hi_p[p] <= cfg->demand_lo_p[p])
+      return fail(SCG_ERR_INVALID, "product %d: demand range (%d, %d) must have lo < hi", p, cfg->demand_lo_p[p],
+                  cfg->demand_hi_p[p]);
+    if ((k == SCG_SC_DEMAND_NORMAL || k == SCG_SC_DEMAND_SINE_NORMAL) && !cfg->demand_thr && !cfg->demand_table)
+      return fail(SCG_ERR_INVALID, "product %d: normal demand needs the threshold table", p);
+    if (k == SCG_SC_DEMAND_SINE_UNIFORM && ((!cfg->demand_base && !cfg->demand_table) || cfg->demand_pert_n[p] < 1))
+      return fail(SCG_ERR_INVALID, "product %d: sinusoidal demand needs the base table and a perturbation range", p);
+  }
   int n_act = 0, n_lt = 0, n_ret = 0;
   for (int i = 0; i < NN; ++i) {
     const scg_sc_node& nd = nodes[i];

@@ -29,10 +29,31 @@ struct ScCtx {
   const int32_t* lt_tab;   // [N][T][n_lt] or null (Philox)
   int32_t n_nodes, P, R, A, O, H, T;
   int32_t avg_lt, max_lt, stochastic, n_lt, lt_thr_len;
-  int32_t lo, hi;
   int32_t pen_unmet, pen_stock, pen_proc, pen_ship;
   uint32_t key0, key1;
+  // per-product demand models (scg_sc_config demand_*; demands_generator.py:3-89)
+  int32_t dkind[SCG_SC_MAX_PRODUCTS], dlo[SCG_SC_MAX_PRODUCTS], dhi[SCG_SC_MAX_PRODUCTS];
+  int32_t dpert_lo[SCG_SC_MAX_PRODUCTS], dpert_n[SCG_SC_MAX_PRODUCTS];
+  int64_t doff[SCG_SC_MAX_PRODUCTS];
+  const uint32_t* dthr;
+  const double* dbase;
 };
+
+// The demand models of a config: per product, or every product uniform on
+// [demand_lo, demand_hi] when the config gives none (host side of the launch).
+inline void sc_ctx_demand(ScCtx& c, const scg_sc_config* cfg) {
+  for (int p = 0; p < SCG_SC_MAX_PRODUCTS; ++p) {
+    const bool m = cfg->demand_models != 0;
+    c.dkind[p] = m ? cfg->demand_kind[p] : SCG_SC_DEMAND_UNIFORM;
+    c.dlo[p] = m ? cfg->demand_lo_p[p] : cfg->demand_lo;
+    c.dhi[p] = m ? cfg->demand_hi_p[p] : cfg->demand_hi;
+    c.dpert_lo[p] = m ? cfg->demand_pert_lo[p] : 0;
+    c.dpert_n[p] = m ? cfg->demand_pert_n[p] : 0;
+    c.doff[p] = m ? cfg->demand_off[p] : 0;
+  }
+  c.dthr = cfg->demand_thr;
+  c.dbase = cfg->demand_base;
+}
 
 // One env's state: element i of a per-env array lives at [i * stride] (stock) or
 // [i * hstride] (heap arrays, which the LDS-staged kernel keeps in shared memory).
@@ -116,14 +137,43 @@ __host__ __device__ __forceinline__ uint32_t cached_word(const ScCtx& c, const S
   return s == 0 ? wc.w.x : s == 1 ? wc.w.y : s == 2 ? wc.w.z : wc.w.w;
 }
 
-// customer_demands[row, r, p] (np.int64): uniform integer in [lo, hi]
+// #{k < n : thr[k] <= u} over a nondecreasing table (upper bound)
+__host__ __device__ __forceinline__ int32_t sc_count_le(const uint32_t* thr, int32_t n, uint32_t u) {
+  int32_t a = 0, b = n;
+  while (a < b) {
+    const int32_t m = (a + b) >> 1;
+    if (thr[m] <= u)
+      a = m + 1;
+    else
+      b = m;
+  }
+  return a;
+}
+
+// customer_demands[row, r, p] (np.int64) of the product's model (envs/demand.py): one
+// Philox word per entry whatever the model.
 __host__ __device__ __forceinline__ int32_t sc_demand(const ScCtx& c, const ScEnv& e, WordCache& wc, int row, int r,
                                                       int p) {
   const uint32_t j = static_cast<uint32_t>((row * c.R + r) * c.P + p);
   if (c.dem_tab) return c.dem_tab[e.local * (static_cast<int64_t>(c.T + 1) * c.R * c.P) + j];
   const uint32_t u = cached_word(c, e, wc, j, SCG_STREAM_SC_DEMAND);
-  const uint64_t span = static_cast<uint64_t>(c.hi - c.lo + 1);
-  return c.lo + static_cast<int32_t>((static_cast<uint64_t>(u) * span) >> 32);
+  const int32_t lo = c.dlo[p], hi = c.dhi[p];
+  switch (c.dkind[p]) {
+    case SCG_SC_DEMAND_NORMAL:  // rint(clip(normal(mean, std))) by its exact CDF (:38-49)
+      return lo + sc_count_le(c.dthr + c.doff[p], hi - lo, u);
+    case SCG_SC_DEMAND_SINE_NORMAL:  // per period: rint(clip(b_t + normal(0, std))) (:51-89)
+      return lo + sc_count_le(c.dthr + c.doff[p] + static_cast<int64_t>(row) * (hi - lo), hi - lo, u);
+    case SCG_SC_DEMAND_SINE_UNIFORM: {  // rint(clip(b_t + randint(-3 std, 3 std + 1))) (:74-86)
+      const int32_t jj = c.dpert_lo[p] + static_cast<int32_t>((static_cast<uint64_t>(u) * static_cast<uint32_t>(c.dpert_n[p])) >> 32);
+      double x = c.dbase[c.doff[p] + row] + static_cast<double>(jj);
+      x = x < lo ? static_cast<double>(lo) : (x > hi ? static_cast<double>(hi) : x);
+      return static_cast<int32_t>(rint(x));
+    }
+    default: {  // randint(lo, hi + 1) (:33-36)
+      const uint64_t span = static_cast<uint64_t>(hi - lo + 1);
+      return lo + static_cast<int32_t>((static_cast<uint64_t>(u) * span) >> 32);
+    }
+  }
 }
 
 // leadtimes[t-1, k]: clip(1 + Poisson(avg-1), 1, max)   (:670-672)
@@ -416,8 +466,9 @@ __host__ __device__ __forceinline__ double sc_obs_norm(double x) {
 template <class Sink>
 __host__ __device__ inline void sc_observe_demand(const ScCtx& c, const ScEnv& e, int t, int k, Sink& out) {
   WordCache dmc{0, U4{0, 0, 0, 0}, false};
-  const double range = static_cast<double>(c.hi - c.lo);
-  out(k, sc_obs_norm(static_cast<double>(sc_demand(c, e, dmc, t, k / c.P, k % c.P) - c.lo) / range));
+  const int p = k % c.P;
+  const double range = static_cast<double>(c.dhi[p] - c.dlo[p]);
+  out(k, sc_obs_norm(static_cast<double>(sc_demand(c, e, dmc, t, k / c.P, p) - c.dlo[p]) / range));
 }
 
 // node i, product p: stock share, then avg_leadtime in-transit bins

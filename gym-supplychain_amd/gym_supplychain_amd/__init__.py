@@ -9,19 +9,19 @@ dynamics run as fused HIP kernels through the C ABI in include/scgpu.h.
     venv = gsa.make_vec("beergame-v0", 65536, demand="poisson", seed=0)   # batched
 """
 from . import _native  # noqa: F401  (fails loudly when libscgpu.so is missing)
-from .envs import (SCENARIOS, BeerGame2VecEnv, BeerGameEnv, BeerGameEnv2, BeerGameVecEnv, SupplyChain2perStageEnv, SupplyChainEnv,
-                   SupplyChainMultiProduct, SupplyChainMultiProduct_IncreasingCosts, SupplyChainNPerStage,
-                   SupplyChainVecEnv)
+from .envs import (SCENARIOS, BeerGame2VecEnv, BeerGameEnv, BeerGameEnv2, BeerGameVecEnv, SupplyChain2perStageEnv,
+                   SupplyChain2perStageSeasonalEnv, SupplyChainEnv, SupplyChainMultiProduct,
+                   SupplyChainMultiProduct_DemConfigByProd, SupplyChainMultiProduct_DemConfigByProd_IncCosts,
+                   SupplyChainMultiProduct_IncreasingCosts, SupplyChainNPerStage, SupplyChainVecEnv)
 from .vec_env import SB3VecEnv
 
 __all__ = ["BeerGameEnv", "BeerGameVecEnv", "BeerGameEnv2", "BeerGame2VecEnv", "SupplyChainEnv", "SupplyChainVecEnv", "SupplyChain2perStageEnv",
            "SupplyChainNPerStage", "SupplyChainMultiProduct", "SupplyChainMultiProduct_IncreasingCosts",
+           "SupplyChain2perStageSeasonalEnv", "SupplyChainMultiProduct_DemConfigByProd",
+           "SupplyChainMultiProduct_DemConfigByProd_IncCosts",
            "SB3VecEnv", "ENV_IDS", "VEC_ENV_IDS", "make", "make_vec", "register_gym"]
 
 # id -> entry point, as registered by the reference (gym_supplychain/__init__.py:3-51).
-# Ids whose demand model is not on the GPU path yet (seasonal / per-product demand
-# configs: sc-2perstage-seasonal-v0, sc-2perstage-multiproduct-v1,
-# sc-2perstage-multiproduct-inccosts-v1) are not registered.
 ENV_IDS = {
     "beergame-v0": "gym_supplychain_amd.envs:BeerGameEnv",
     "beergame-v2": "gym_supplychain_amd.envs:BeerGameEnv2",
@@ -30,6 +30,9 @@ ENV_IDS = {
     "sc-2perstage-multiproduct-v0": "gym_supplychain_amd.envs:SupplyChainMultiProduct",
     "sc-Nperstage-multiproduct-v0": "gym_supplychain_amd.envs:SupplyChainNPerStage",
     "sc-2perstage-multiproduct-inccosts-v0": "gym_supplychain_amd.envs:SupplyChainMultiProduct_IncreasingCosts",
+    "sc-2perstage-seasonal-v0": "gym_supplychain_amd.envs:SupplyChain2perStageSeasonalEnv",
+    "sc-2perstage-multiproduct-v1": "gym_supplychain_amd.envs:SupplyChainMultiProduct_DemConfigByProd",
+    "sc-2perstage-multiproduct-inccosts-v1": "gym_supplychain_amd.envs:SupplyChainMultiProduct_DemConfigByProd_IncCosts",
 }
 _VEC_KEYS = ("seed", "device", "env_offset", "auto_reset", "obs_dtype", "track_returns", "kernel", "demand_table",
              "leadtime_table")

@@ -138,7 +138,11 @@ class ScConfig(ctypes.Structure):
         ("leadtime_table", ctypes.c_void_p)] + [
         (f, ctypes.c_int32) for f in ("kernel", "layout", "group", "n_levels")] + [
         ("level_start", ctypes.c_int32 * (SC_MAX_LEVELS + 1)), ("inbox_size", ctypes.c_int32),
-        ("level_staged", ctypes.c_int32)]
+        ("level_staged", ctypes.c_int32), ("demand_models", ctypes.c_int32)] + [
+        (f, ctypes.c_int32 * SC_MAX_PRODUCTS) for f in ("demand_kind", "demand_lo_p", "demand_hi_p",
+                                                        "demand_pert_lo", "demand_pert_n")] + [
+        ("demand_off", ctypes.c_int64 * SC_MAX_PRODUCTS), ("demand_thr", ctypes.c_void_p),
+        ("demand_base", ctypes.c_void_p)]
 
 
 class ScState(ctypes.Structure):

@@ -61,6 +61,18 @@ def two_per_stage_nodes(**kw):
     return stage, _env_kwargs(c)
 
 
+# ---- sc-2perstage-seasonal-v0 (supplychain_2perstage_env.py:67-97) ------------------------
+SEASONAL_DEFAULTS = dict(
+    TWO_PER_STAGE_DEFAULTS, initial_stocks=[800] * 8, initial_supply=[[[600, 600]], [[840, 840]]],
+    initial_shipments=[[[600, 600]], [[840, 840]]] + [[[240, 240]]] * 4, supply_capacities=[600, 840],
+    processing_capacities=[840, 960], stock_capacities=[1600, 1800] * 4, ship_capacity=1800,
+    demand_range=(0, 400), demand_std=10, demand_sen_peaks=4, avg_demand_range=(150, 250), demand_perturb_norm=True)
+
+
+def two_per_stage_seasonal_nodes(check_actions=False, **kw):
+    return two_per_stage_nodes(**dict(SEASONAL_DEFAULTS, **kw))
+
+
 # ---- sc-Nperstage-multiproduct-v0 / ntom (supplychain_Nperstage_env.py:3-131) -------------
 N_PER_STAGE_DEFAULTS = dict(
     nodes_per_echelon=3, num_products=2, initial_stocks=None, stock_capacities=None, stock_costs=1,
@@ -187,11 +199,34 @@ def increasing_costs_kwargs(num_products=2, **kw):
                 stock_costs=[1 * (i + 1) for i in range(P)])
 
 
+def by_product_demand_kwargs(num_products=2, demand_std=None, demand_perturb_norm=False, inc_costs=False, **kw):
+    """SupplyChainMultiProduct_DemConfigByProd(_IncCosts) (supplychain_multiproduct_env.py:157-274):
+    product 1 seasonal (0..400, 4 peaks, mean 100..300), product 2 regular (0..300),
+    product 3 seasonal (0..400, 2 peaks); at most 3 products."""
+    P = num_products
+    if not 1 <= P <= 3:
+        raise AssertionError("at most 3 products (supplychain_multiproduct_env.py:174)")
+    # the _IncCosts variant appends [demand_std] (a list) for products 2 and 3 (:243, :250)
+    later_std = [demand_std] if inc_costs else demand_std
+    ranges, stds, peaks, avg = [(0, 400)], [demand_std], [4], [(100, 300)]
+    if P > 1:
+        ranges.append((0, 300)), stds.append(later_std), peaks.append(None), avg.append(None)
+    if P > 2:
+        ranges.append((0, 400)), stds.append(later_std), peaks.append(2), avg.append((100, 300))
+    out = dict(kw, num_products=P, demand_config_by_product=True, demand_range=ranges, demand_std=stds,
+               demand_sen_peaks=peaks, avg_demand_range=avg, demand_perturb_norm=[demand_perturb_norm] * P)
+    return increasing_costs_kwargs(**out) if inc_costs else out
+
+
 SCENARIOS = {
     "sc-2perstage-v0": two_per_stage_nodes,
     "sc-Nperstage-multiproduct-v0": n_per_stage_nodes,
     "sc-2perstage-multiproduct-v0": multi_product_nodes,
     "sc-2perstage-multiproduct-inccosts-v0": lambda **kw: multi_product_nodes(**increasing_costs_kwargs(**kw)),
+    "sc-2perstage-seasonal-v0": two_per_stage_seasonal_nodes,
+    "sc-2perstage-multiproduct-v1": lambda **kw: multi_product_nodes(**by_product_demand_kwargs(**kw)),
+    "sc-2perstage-multiproduct-inccosts-v1":
+        lambda **kw: multi_product_nodes(**by_product_demand_kwargs(inc_costs=True, **kw)),
 }
 
 
@@ -219,3 +254,18 @@ class SupplyChainMultiProduct(_Scenario):
 
 class SupplyChainMultiProduct_IncreasingCosts(_Scenario):
     _builder = staticmethod(lambda **kw: multi_product_nodes(**increasing_costs_kwargs(**kw)))
+
+
+class SupplyChain2perStageSeasonalEnv(_Scenario):
+    """sc-2perstage-seasonal-v0: 2-per-stage chain, sinusoidal demand with normal perturbation."""
+    _builder = staticmethod(two_per_stage_seasonal_nodes)
+
+
+class SupplyChainMultiProduct_DemConfigByProd(_Scenario):
+    """sc-2perstage-multiproduct-v1: demand configured per product."""
+    _builder = staticmethod(lambda **kw: multi_product_nodes(**by_product_demand_kwargs(**kw)))
+
+
+class SupplyChainMultiProduct_DemConfigByProd_IncCosts(_Scenario):
+    """sc-2perstage-multiproduct-inccosts-v1: per-product demand and increasing costs."""
+    _builder = staticmethod(lambda **kw: multi_product_nodes(**by_product_demand_kwargs(inc_costs=True, **kw)))

@@ -28,6 +28,7 @@ import torch
 
 from .. import _native as nat
 from .. import spaces
+from . import demand
 
 _MAXP = nat.SC_MAX_PRODUCTS
 _MAXD = nat.SC_MAX_DESTS
@@ -68,21 +69,26 @@ class SupplyChainSpec:
                  demand_config_by_product=False, demand_range=(10, 20), demand_std=None, demand_sen_peaks=None,
                  avg_demand_range=None, processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2,
                  max_leadtime=2, total_time_steps=360, seed=None, build_info=False, demand_perturb_norm=False):
-        if demand_config_by_product:
-            raise NotImplementedError("demand_config_by_product=True is not supported on the GPU path yet")
-        if demand_std is not None or demand_sen_peaks is not None:
-            raise NotImplementedError("only uniform demand (demand_std=None, demand_sen_peaks=None) is supported yet")
         self.build_info = bool(build_info)
         P = _int("num_products", num_products)
         if not 1 <= P <= _MAXP:
             raise ValueError(f"num_products={P} outside 1..{_MAXP}")
-        lo, hi = demand_range
-        if lo == hi:
-            raise AssertionError("demand_range must not be empty")  # :592
         self.P = P
-        self.demand_range = (_int("demand_range[0]", lo), _int("demand_range[1]", hi))
-        if self.demand_range[1] < self.demand_range[0]:
-            raise ValueError("demand_range must be (low, high) with low < high")
+        self.demand_config_by_product = bool(demand_config_by_product)
+        ranges = list(demand_range) if demand_config_by_product else [demand_range] * P
+        if len(ranges) != P:
+            raise AssertionError("demand_range needs one (low, high) per product")
+        for lo, hi in ranges:
+            if lo == hi:
+                raise AssertionError("demand_range must not be empty")  # :592-595
+            if _int("demand_range[1]", hi) < _int("demand_range[0]", lo):
+                raise ValueError("demand_range must be (low, high) with low < high")
+        self.demand_range = tuple(ranges[0]) if not demand_config_by_product else [tuple(r) for r in ranges]
+        # per-product generators (demands_generator.py:3-89; envs/demand.py)
+        self.demand_models = demand.models_for(dict(
+            demand_config_by_product=demand_config_by_product, demand_range=demand_range, demand_std=demand_std,
+            demand_sen_peaks=demand_sen_peaks, avg_demand_range=avg_demand_range,
+            demand_perturb_norm=demand_perturb_norm), P)
         self.penalties = dict(unmet_demand_cost=_int("unmet_demand_cost", unmet_demand_cost),
                               exceeded_stock_capacity_cost=_int("exceeded_stock_capacity_cost",
                                                                 exceeded_stock_capacity_cost),
@@ -256,7 +262,10 @@ class SupplyChainVecEnv:
         c.total_time_steps = spec.total_time_steps
         c.avg_leadtime, c.max_leadtime = spec.avg_leadtime, spec.max_leadtime
         c.stochastic_leadtimes = int(spec.stochastic_leadtimes)
-        c.demand_lo, c.demand_hi = spec.demand_range
+        models = spec.demand_models
+        c.demand_lo, c.demand_hi = models[0].lo, models[0].hi
+        if any(m.kind != demand.UNIFORM or (m.lo, m.hi) != (models[0].lo, models[0].hi) for m in models):
+            self._demand_tables(c, models, spec.total_time_steps)
         for k, v in spec.penalties.items():
             setattr(c, k, v)
         c.obs_f64 = int(obs_dtype == torch.float64)
@@ -344,6 +353,17 @@ class SupplyChainVecEnv:
                                                         self._term_obs.data_ptr())
         self.single_action_space = spaces.Box(-1.0, 1.0, (c.n_actions,), np.float32)          # :625
         self.single_observation_space = spaces.Box(-1.0, 1.0, (c.n_obs,), np.float32)         # :626
+
+    def _demand_tables(self, c, models, T):
+        """Per-product demand models into the config; their tables onto the device."""
+        self._dem_tabs = []
+
+        def upload(a):
+            t = torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).to(self.device)
+            self._dem_tabs.append(t)
+            return t.data_ptr()
+
+        demand.fill_config(c, models, T, upload)
 
     def _stream(self):
         return nat.raw_stream(self._dev_index)

@@ -79,7 +79,7 @@ class SB3VecEnv(_SB3VecEnv):
         if actions is None:
             raise RuntimeError("step_wait() without step_async()")
         obs, rew, done, info = self.venv.step(actions)
-        terminal = bool(info)
+        terminal = "terminal_observation" in info  # build_info puts 'sc_episode' in every info
         if not self.numpy:
             infos = self._infos(terminal, info, device=True)
             return obs, rew, done, infos

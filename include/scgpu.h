@@ -284,7 +284,25 @@ typedef struct scg_sc_config {
   int32_t level_start[SCG_SC_MAX_LEVELS + 1];
   int32_t inbox_size;           /* out: shipment inbox entries per env (level kernel)       */
   int32_t level_staged;         /* out: 1 = the level kernel stages each env's state in LDS */
+  /* Per-product demand models (demands_generator.py:3-89). demand_models = 0: every
+   * product is uniform on [demand_lo, demand_hi]. Otherwise per product p: kind
+   * SCG_SC_DEMAND_*, range [lo_p, hi_p] (also the observation's normalisation, :771-777),
+   * NORMAL / SINE_NORMAL: a draw is lo_p + #{k : thr[off_p + row * (hi_p - lo_p) + k] <= u}
+   * (row 0 for NORMAL, the period for SINE_NORMAL); SINE_UNIFORM: rint(clip(base[off_p +
+   * period] + j, lo_p, hi_p)) with j = pert_lo_p + floor(u * pert_n_p / 2^32). */
+  int32_t demand_models;
+  int32_t demand_kind[SCG_SC_MAX_PRODUCTS];
+  int32_t demand_lo_p[SCG_SC_MAX_PRODUCTS], demand_hi_p[SCG_SC_MAX_PRODUCTS];
+  int32_t demand_pert_lo[SCG_SC_MAX_PRODUCTS], demand_pert_n[SCG_SC_MAX_PRODUCTS];
+  int64_t demand_off[SCG_SC_MAX_PRODUCTS];
+  const uint32_t* demand_thr;   /* DEVICE thresholds of the NORMAL / SINE_NORMAL products  */
+  const double* demand_base;    /* DEVICE [T+1] sinusoid bases of the SINE_UNIFORM products */
 } scg_sc_config;
+
+#define SCG_SC_DEMAND_UNIFORM 0
+#define SCG_SC_DEMAND_NORMAL 1
+#define SCG_SC_DEMAND_SINE_NORMAL 2
+#define SCG_SC_DEMAND_SINE_UNIFORM 3
 
 /* Batch state. NP = n_nodes * n_products; per-env arrays follow cfg->layout (shapes below
  * are the env-fastest ones; env-major puts the env index first). */

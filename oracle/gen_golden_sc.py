@@ -26,7 +26,7 @@ OUT = os.path.join(REPO, "tests", "golden")
 sys.dont_write_bytecode = True
 sys.path.insert(0, REPO)
 
-from oracle.sc_draws import sc_demand_table, sc_leadtime_table  # noqa: E402
+from oracle.sc_draws import sc_demand_table, sc_demand_table_models, sc_leadtime_table  # noqa: E402
 
 # Amount type codes in recorded heaps (amounts are float32, float64 or int)
 KIND = {int: 0, float: 1, np.float32: 2, np.float64: 3, np.int64: 4}
@@ -60,7 +60,31 @@ CASES = {
     # multi-product 2-per-stage factory (config only in the reference)
     "multiproduct": dict(factory="SupplyChainMultiProduct", kwargs=dict(total_time_steps=30), n_envs=4,
                          act="uniform", seed=17),
+    # sc-2perstage-seasonal-v0: sinusoidal demand with normal perturbation (demands_generator.py:51-89)
+    "seasonal": dict(factory="SupplyChain2perStageSeasonalEnv", kwargs=dict(total_time_steps=40), n_envs=4,
+                     act="uniform", seed=18),
+    # sc-2perstage-multiproduct-v1: demand configured per product (sinusoid, uniform and a
+    # second sinusoid, uniform perturbation; per-product observation normalisation)
+    "byproduct": dict(factory="SupplyChainMultiProduct_DemConfigByProd",
+                      kwargs=dict(num_products=3, demand_std=6, total_time_steps=30), n_envs=4, act="uniform",
+                      seed=19),
+    # the same with normal perturbations and normal (non-sinusoidal) product 2
+    "byproduct_normal": dict(factory="SupplyChainMultiProduct_DemConfigByProd",
+                             kwargs=dict(num_products=2, demand_std=25.0, demand_perturb_norm=True,
+                                         total_time_steps=30), n_envs=4, act="uniform", seed=20),
 }
+
+
+def demand_models(env):
+    """Per-product generator settings of a reference env (:566-590), oracle/sc_draws form."""
+    P = env.num_products
+    if not env.demand_config_by_product:
+        m = dict(lo=env.demand_range[0], hi=env.demand_range[1], std=env.demand_std, sen_peaks=env.demand_sen_peaks,
+                 minavg=env.minavg_demand, maxavg=env.maxavg_demand, perturb_norm=env.demand_perturb_norm)
+        return [m] * P
+    return [dict(lo=env.demand_range[p][0], hi=env.demand_range[p][1], std=env.demand_std[p],
+                 sen_peaks=env.demand_sen_peaks[p], minavg=env.minavg_demand[p], maxavg=env.maxavg_demand[p],
+                 perturb_norm=env.demand_perturb_norm[p]) for p in range(P)]
 
 
 def _capture_init(mod):
@@ -122,7 +146,7 @@ def run_case(name, spec):
     H = 64
     rng = np.random.RandomState(spec["seed"])
     seed = 1000 + spec["seed"]
-    lo, hi = env.demand_range
+    models = demand_models(env)
     rec = dict(obs=np.zeros((T + 1, N, n_obs)), reward=np.zeros((T, N)),
                stock=np.zeros((T + 1, N, len(env.nodes), P)),
                heap_t=np.zeros((T + 1, N, len(env.nodes), P, H), dtype=np.int32),
@@ -144,8 +168,12 @@ def run_case(name, spec):
     for n in range(N):
         env.seed(n)
         env.reset()
-        dem = sc_demand_table(seed, n, 0, T, R, P, lo, hi)
-        env.customer_demands = dem.copy()
+        if all(m["std"] is None and m["sen_peaks"] is None for m in models) and not env.demand_config_by_product:
+            dem = sc_demand_table(seed, n, 0, T, R, P, models[0]["lo"], models[0]["hi"])
+        else:
+            dem = sc_demand_table_models(seed, n, 0, T, R, P, models)
+        # by product the reference keeps one (T+1, R) table per product (:655-661)
+        env.customer_demands = [dem[:, :, p].copy() for p in range(P)] if env.demand_config_by_product else dem.copy()
         rec["demands"][n] = dem
         if n_lt:
             lts = sc_leadtime_table(seed, n, 0, T, n_lt, env.avg_leadtime, env.max_leadtime)
@@ -175,7 +203,7 @@ def run_case(name, spec):
     for k in ("heap_t", "heap_v", "heap_k"):
         rec[k] = rec[k][..., :max(used, 1)]
     meta = dict(factory=spec["factory"], factory_kwargs=spec["kwargs"], nodes_info=seen["nodes_info"],
-                kwargs=seen["kwargs"], T=T, R=R, P=P, n_act=n_act, n_obs=n_obs, n_lt=n_lt, seed=seed,
+                kwargs=seen["kwargs"], demand_models=models, T=T, R=R, P=P, n_act=n_act, n_obs=n_obs, n_lt=n_lt, seed=seed,
                 node_names=[nd.label for nd in env.nodes])
     return rec, meta
 

@@ -245,7 +245,7 @@ class SupplyChainOracle:
     def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
                  exceeded_process_capacity_cost=1000, exceeded_ship_capacity_cost=1000, demand_range=(10, 20),
                  processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2, max_leadtime=2,
-                 total_time_steps=360, build_info=False):
+                 total_time_steps=360, build_info=False, demand_config_by_product=False):
         P = num_products
         self.build_info = build_info
         pens = (exceeded_stock_capacity_cost, exceeded_process_capacity_cost, exceeded_ship_capacity_cost,
@@ -263,9 +263,11 @@ class SupplyChainOracle:
         self.retailers = [nd for nd in self.nodes if nd.last_level]
         self.P = P
         self.T = total_time_steps
-        self.lo, self.hi = demand_range
-        if self.lo == self.hi:
-            raise AssertionError("demand_range must not be empty")             # :592
+        ranges = list(demand_range) if demand_config_by_product else [demand_range] * P   # :566-595
+        self.lo = np.array([r[0] for r in ranges], dtype=np.int64)
+        self.hi = np.array([r[1] for r in ranges], dtype=np.int64)
+        if (self.lo == self.hi).any():
+            raise AssertionError("demand_range must not be empty")             # :592-595
         self.stochastic = stochastic_leadtimes
         self.avg_lt = avg_leadtime
         self.max_lt = max_leadtime
@@ -326,7 +328,8 @@ class SupplyChainOracle:
         return self._obs(), reward, self.t == self.T, info
 
     def _obs(self):                                                           # :762-791
-        dem = (self.demands[self.t, :].flatten() - self.lo) / (self.hi - self.lo)
+        # per retailer, per product: (d - low_p) / range_p (:771-777)
+        dem = ((self.demands[self.t] - self.lo) / (self.hi - self.lo)).flatten()
         nodes = []
         for nd in self.nodes:
             nodes += _node_obs(nd, self.t + 1, self.t + self.avg_lt)

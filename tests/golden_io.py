@@ -27,7 +27,7 @@ def load_beergame(name):
 # ---- SupplyChain (written by oracle/gen_golden_sc.py) ----------------------------------
 SC_ORACLE_KW = ("num_products", "unmet_demand_cost", "exceeded_stock_capacity_cost", "exceeded_process_capacity_cost",
                 "exceeded_ship_capacity_cost", "demand_range", "processing_ratio", "stochastic_leadtimes",
-                "avg_leadtime", "max_leadtime", "total_time_steps")
+                "avg_leadtime", "max_leadtime", "total_time_steps", "demand_config_by_product")
 
 
 def sc_cases():

@@ -41,8 +41,7 @@ static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node*
   c.stochastic = cfg->stochastic_leadtimes;
   c.n_lt = cfg->n_leadtimes;
   c.lt_thr_len = cfg->leadtime_poisson_len;
-  c.lo = cfg->demand_lo;
-  c.hi = cfg->demand_hi;
+  scg::sc_ctx_demand(c, cfg);
   c.pen_unmet = cfg->unmet_demand_cost;
   c.pen_stock = cfg->exceeded_stock_capacity_cost;
   c.pen_proc = cfg->exceeded_process_capacity_cost;

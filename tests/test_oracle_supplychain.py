@@ -21,7 +21,7 @@ CASES = sc_cases()
 
 def test_golden_present():
     assert {"2perstage", "2perstage_full", "2perstage_stoch", "2perstage_edges", "ntom", "nperstage_3p_stoch",
-            "multiproduct"} <= set(CASES)
+            "multiproduct", "seasonal", "byproduct", "byproduct_normal"} <= set(CASES)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -54,7 +54,11 @@ def test_scenario_builders_match_reference(name):
     meta = g["meta"]
     builder = {"SupplyChain2perStageEnv": scenarios.two_per_stage_nodes,
                "SupplyChainNPerStage": scenarios.n_per_stage_nodes,
-               "SupplyChainMultiProduct": scenarios.multi_product_nodes}[meta["factory"]]
+               "SupplyChainMultiProduct": scenarios.multi_product_nodes,
+               "SupplyChain2perStageSeasonalEnv": scenarios.two_per_stage_seasonal_nodes,
+               "SupplyChainMultiProduct_DemConfigByProd":
+                   lambda **kw: scenarios.multi_product_nodes(**scenarios.by_product_demand_kwargs(**kw)),
+               }[meta["factory"]]
     nodes, kw = builder(**meta["factory_kwargs"])
     assert json.loads(json.dumps(nodes)) == meta["nodes_info"]
     ref_kw = json.loads(json.dumps(meta["kwargs"]))

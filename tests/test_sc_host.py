@@ -29,7 +29,18 @@ def _setup(g, kernel=0):
     c.n_nodes, c.n_products, c.n_retailers = len(spec.nodes), spec.P, spec.n_retailers
     c.total_time_steps, c.avg_leadtime, c.max_leadtime = spec.total_time_steps, spec.avg_leadtime, spec.max_leadtime
     c.stochastic_leadtimes = int(spec.stochastic_leadtimes)
-    c.demand_lo, c.demand_hi = spec.demand_range
+    from gym_supplychain_amd.envs import demand
+    models = spec.demand_models
+    c.demand_lo, c.demand_hi = models[0].lo, models[0].hi
+    keep = []
+
+    def host_upload(a):  # the host build reads the model tables from host memory
+        keep.append(a)
+        return a.ctypes.data
+
+    if any(m.kind != demand.UNIFORM or (m.lo, m.hi) != (models[0].lo, models[0].hi) for m in models):
+        demand.fill_config(c, models, spec.total_time_steps, host_upload)
+    c._keep = keep
     for k, v in spec.penalties.items():
         setattr(c, k, v)
     thr = None
