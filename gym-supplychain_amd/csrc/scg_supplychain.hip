@@ -16,6 +16,7 @@
 #include "scg_common.h"
 #include "scg_supplychain_core.h"
 #include "scg_supplychain_level.h"
+#include "scg_supplychain_staged.h"
 #include "scgpu.h"
 
 namespace scg {
@@ -35,6 +36,8 @@ struct ScArgs {
   double* ep_ret;
   double* final_ret;
   int32_t* err;
+  int32_t* inbox_tk;  // staged kernel: shipment inbox [inbox_size][N]
+  double* inbox_val;
   double* led_v;     // build_info ledgers [2*8*P][N] (lane kernels) or null
   int32_t* led_k;
   double* led_fv;    // terminal-step ledger on auto-reset
@@ -203,6 +206,64 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
       a.val[g] = lval[(hp * c.H + j) * kScBlock + lane];
     }
   }
+}
+
+// Node-staged step (scg_supplychain_staged.h): one lane per env; the heaps of the node being
+// processed are staged in LDS ([product][slot][lane], lane fastest: conflict free), the
+// shipments go through the env's HBM inbox, the node's observation is written while its
+// heaps are staged. No block-wide barrier: every lane only touches its own LDS column.
+template <int MAXD>
+__global__ __launch_bounds__(kScBlock) void sc_step_staged_kernel(const ScArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + lane;
+  if (n >= a.n) return;
+  const ScCtx& c = a.c;
+  const int slots = c.P * c.H;
+  double* lval = reinterpret_cast<double*>(smem);
+  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
+  int32_t* lsize = ltk + static_cast<int64_t>(slots) * kScBlock;
+  ScEnv g = env_view(a, n, a.episode);
+  ScEnv loc = g;
+  loc.tk = ltk + lane;
+  loc.val = lval + lane;
+  loc.size = lsize + lane;
+  loc.hstride = kScBlock;
+  const StagedInbox in{a.inbox_tk + n, a.inbox_val + n, a.n};
+  const bool terminal = a.flags & 1;
+  const bool autoreset = a.flags & 2;
+  // node observations go to obs, or to the terminal observation when the env resets now
+  void* node_obs = autoreset ? a.term_obs : a.obs;
+  ObsRow main{node_obs ? node_obs : a.obs, n * c.O, a.obs_f64};
+  ObsRow extra{a.term_obs, n * c.O, a.obs_f64};
+  const bool both = terminal && !autoreset && a.term_obs;
+  auto sink = [&](int o, double x) {
+    if (node_obs) main(o, x);
+    if (both) extra(o, x);
+  };
+  const double reward = sc_staged_step<MAXD>(c, g, loc, in, a.act + n * c.A, a.t, sink);
+  a.rew[n] = reward;
+  if (a.ep_ret) {
+    const double r = a.ep_ret[n] + reward;
+    if (terminal && a.final_ret) a.final_ret[n] = r;
+    a.ep_ret[n] = autoreset ? 0.0 : r;
+  }
+  auto rest = [&](ObsRow& row, int t) {  // demand and time-to-go elements (:771, :786)
+    for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, t, k, row);
+    sc_observe_tail(c, t, row);
+  };
+  if (autoreset) {
+    if (a.term_obs) rest(extra, a.t);
+    snapshot_ledger(a, c, n);
+    g.episode = a.episode + 1;
+    sc_reset_env(c, g);
+    ObsRow out{a.obs, n * c.O, a.obs_f64};
+    sc_observe(c, g, 0, out);
+  } else {
+    rest(main, a.t);
+    if (both) rest(extra, a.t);
+  }
+  if (g.overflow) atomicOr(a.err, 1);
 }
 
 // Level-parallel step (scg_supplychain_level.h): G lanes per env, 64 / G envs per block,
@@ -390,6 +451,8 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   a.ep_ret = st->episode_return;
   a.final_ret = st->final_return;
   a.err = st->error_flags;
+  a.inbox_tk = st->inbox_tk;
+  a.inbox_val = st->inbox_val;
   a.led_v = st->ledger;
   a.led_k = st->ledger_kind;
   a.led_fv = st->final_ledger;
@@ -467,6 +530,40 @@ size_t sc_lds_bytes(const scg_sc_config* cfg) {
   const size_t NP = static_cast<size_t>(cfg->n_nodes) * cfg->n_products;
   return kScBlock * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
 }
+// Staged kernel: one node's heaps per lane.
+size_t sc_staged_lds_bytes(const scg_sc_config* cfg) {
+  return kScBlock * static_cast<size_t>(cfg->n_products) * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
+}
+
+// The staged kernel's inbox (scg_supplychain_staged.h): every shipment must go to a later
+// node, at most once per destination list. Fills in_deg/in_base/in_slot/in_stride and
+// returns the entries per env, or -1 when the chain does not qualify.
+int sc_inbox_layout(const scg_sc_config* cfg, scg_sc_node* nodes) {
+  const int NN = cfg->n_nodes, P = cfg->n_products;
+  std::vector<int> deg(NN, 0);
+  for (int i = 0; i < NN; ++i)
+    for (int d = 0; d < nodes[i].n_dests; ++d) {
+      const int j = nodes[i].dests[d];
+      if (j <= i) return -1;
+      for (int d2 = 0; d2 < d; ++d2)
+        if (nodes[i].dests[d2] == j) return -1;
+      ++deg[j];
+    }
+  int base = 0;
+  for (int j = 0; j < NN; ++j) {
+    nodes[j].in_deg = deg[j];
+    nodes[j].in_base = base;
+    base += deg[j] * P;
+  }
+  std::vector<int> next(NN, 0);  // sources enumerated in node order
+  for (int i = 0; i < NN; ++i)
+    for (int d = 0; d < nodes[i].n_dests; ++d) {
+      const int j = nodes[i].dests[d];
+      nodes[i].in_slot[d] = nodes[j].in_base + next[j]++;
+      nodes[i].in_stride[d] = nodes[j].in_deg;
+    }
+  return base;
+}
 
 }  // namespace
 }  // namespace scg
@@ -482,7 +579,7 @@ int scg_sc_struct_sizes(size_t* node_size, size_t* config_size, size_t* state_si
   return SCG_OK;
 }
 
-int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
+int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   if (!cfg || !nodes) return fail(SCG_ERR_INVALID, "null config/node table");
   const int NN = cfg->n_nodes, P = cfg->n_products;
   if (NN < 1 || NN > SCG_SC_MAX_NODES) return fail(SCG_ERR_INVALID, "n_nodes=%d outside 1..%d", NN, SCG_SC_MAX_NODES);
@@ -572,12 +669,24 @@ int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* nodes) {
   // kernel: the lane kernel unless the level-parallel one is asked for (it is the slower
   // of the two on the reference's chains as measured on MI355X)
   const int want = cfg->kernel;
-  if (want != SCG_SC_KERNEL_AUTO && want != SCG_SC_KERNEL_LANE && want != SCG_SC_KERNEL_LEVEL)
+  if (want != SCG_SC_KERNEL_AUTO && want != SCG_SC_KERNEL_LANE && want != SCG_SC_KERNEL_LEVEL &&
+      want != SCG_SC_KERNEL_STAGED)
     return fail(SCG_ERR_INVALID, "kernel=%d is not a SCG_SC_KERNEL_* value", want);
   cfg->n_levels = 0;
   cfg->group = 1;
   cfg->inbox_size = 0;
   cfg->level_staged = 0;
+  if (want == SCG_SC_KERNEL_STAGED) {
+    const int entries = sc_inbox_layout(cfg, nodes);
+    if (entries < 0)
+      return fail(SCG_ERR_INVALID, "the staged kernel needs every shipment to go to a later node, once per list");
+    if (sc_staged_lds_bytes(cfg) > kScLdsMax)
+      return fail(SCG_ERR_INVALID, "one node's heaps (%d products x %d slots) exceed the staged kernel's LDS", P, H);
+    cfg->inbox_size = entries;
+    cfg->kernel = SCG_SC_KERNEL_STAGED;
+    cfg->layout = SCG_SC_LAYOUT_ENV_FASTEST;
+    return SCG_OK;
+  }
   const bool levels = want == SCG_SC_KERNEL_LEVEL && sc_level_schedule(cfg, nodes);
   if (want == SCG_SC_KERNEL_LEVEL && !levels)
     return fail(SCG_ERR_INVALID, "the chain has no level schedule (shipments must go to the next run of nodes)");
@@ -640,6 +749,17 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
       default: SCG_LEVEL_LAUNCH(32); break;
     }
 #undef SCG_LEVEL_LAUNCH
+  } else if (cfg->kernel == SCG_SC_KERNEL_STAGED) {
+    if (!st->inbox_tk || !st->inbox_val || cfg->inbox_size < 0)
+      return fail(SCG_ERR_INVALID, "the staged kernel needs the inbox buffers [inbox_size][N]");
+    const size_t slds = sc_staged_lds_bytes(cfg);
+    switch (sc_maxd_bucket(cfg->max_dests)) {
+      case 2: hipLaunchKernelGGL(sc_step_staged_kernel<2>, grid, dim3(kScBlock), slds, s, a); break;
+      case 4: hipLaunchKernelGGL(sc_step_staged_kernel<4>, grid, dim3(kScBlock), slds, s, a); break;
+      case 8: hipLaunchKernelGGL(sc_step_staged_kernel<8>, grid, dim3(kScBlock), slds, s, a); break;
+      case 16: hipLaunchKernelGGL(sc_step_staged_kernel<16>, grid, dim3(kScBlock), slds, s, a); break;
+      default: hipLaunchKernelGGL(sc_step_staged_kernel<32>, grid, dim3(kScBlock), slds, s, a); break;
+    }
   } else if (cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST) {
     return fail(SCG_ERR_INVALID, "lane kernel needs the env-fastest layout");
   } else if (lds <= kScLdsMax) {

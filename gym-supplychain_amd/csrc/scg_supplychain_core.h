@@ -72,6 +72,7 @@ struct ScEnv {
   double* led_v = nullptr;
   int32_t* led_k = nullptr;
   int64_t led_stride = 0;
+  int32_t hnode0 = 0;  // first node whose heaps the heap arrays hold (staged kernel: the current one)
 };
 
 // info['sc_episode'] categories in the reference's dict order (:416-417)
@@ -106,12 +107,12 @@ __host__ __device__ inline void sc_reset_ledger(const ScCtx& c, ScEnv& e) {
 }
 
 __host__ __device__ __forceinline__ HeapView sc_heap(const ScCtx& c, const ScEnv& e, int node, int p) {
-  const int64_t hp = static_cast<int64_t>(node) * c.P + p;
+  const int64_t hp = static_cast<int64_t>(node - e.hnode0) * c.P + p;
   return HeapView{e.tk + hp * c.H * e.hstride, e.val + hp * c.H * e.hstride, e.hstride};
 }
 
 __host__ __device__ __forceinline__ int32_t& sc_size(const ScCtx& c, const ScEnv& e, int node, int p) {
-  return e.size[(static_cast<int64_t>(node) * c.P + p) * e.hstride];
+  return e.size[(static_cast<int64_t>(node - e.hnode0) * c.P + p) * e.hstride];
 }
 
 __host__ __device__ __forceinline__ double& sc_stock(const ScCtx& c, const ScEnv& e, int node, int p) {
@@ -202,9 +203,12 @@ __host__ __device__ __forceinline__ void sc_push(const ScCtx& c, ScEnv& e, int n
 // Where SHIP pushes go (:347): straight into the destination heap when one lane walks the
 // whole chain in node order (sc_step_env), or into a level inbox that the destination's
 // lane drains in source order before its own act (scg_supplychain_level.h).
+// A Push also says whether the per-destination loop of SHIP unrolls (a plain store per
+// destination does; a heap push keeps the loop rolled to bound code size).
 struct DirectPush {
-  __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv& e, int /*src*/, int dest, int p, int32_t time,
-                                                Num amount) const {
+  static constexpr bool kUnroll = false;
+  __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv& e, int /*src*/, int /*d*/, int dest, int p,
+                                                int32_t time, Num amount) const {
     sc_push(c, e, dest, p, time, amount);
   }
 };
@@ -377,7 +381,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         // destination at a time, every accumulator seeing the reference's order, and no
         // per-destination array besides the split's output stays live.
         Num leaving = pyint(0), ship_cost = pyint(0), ship_units = pyint(0);
-        for (int i = 0; i < D; ++i) {  // rolled: the body holds a heap push
+        auto dest_step = [&](int i) {
           Num o = out.get_dyn(i);
           Num snt = o;  // amounts_to_ship = amounts.copy() (:292)
           if (factory) {
@@ -399,9 +403,16 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
           }
           leaving = np_add(leaving, o);
           if (np_lt(pyint(0), snt))
-            push.ship(c, e, ni, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
+            push.ship(c, e, ni, i, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
           ship_cost = np_add(ship_cost, np_mul(snt, pyint(nd.dest_costs[p][i])));
           ship_units = np_add(ship_units, snt);  // sum(amounts_to_ship) (:356)
+        };
+        if constexpr (Push::kUnroll) {  // every index static: the NumVecs stay in registers
+#pragma unroll
+          for (int i = 0; i < MAXD; ++i)
+            if (i < D) dest_step(i);
+        } else {
+          for (int i = 0; i < D; ++i) dest_step(i);
         }
         double& st = sc_stock(c, e, ni, p);
         st = st - leaving.v;  // float64 array element minus the promoted scalar (:332)

@@ -40,7 +40,8 @@ struct LevelInbox {
   double* val;
   int32_t src0, dst0, wsrc, wdst;
 
-  __host__ __device__ __forceinline__ void ship(const ScCtx&, ScEnv&, int src, int dest, int p, int32_t time,
+  static constexpr bool kUnroll = true;  // an LDS store per destination
+  __host__ __device__ __forceinline__ void ship(const ScCtx&, ScEnv&, int src, int /*d*/, int dest, int p, int32_t time,
                                                 Num amount) const {
     const int idx = (p * wsrc + (src - src0)) * wdst + (dest - dst0);
     tk[idx] = he_pack(time, amount.k);

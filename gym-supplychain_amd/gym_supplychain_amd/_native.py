@@ -103,7 +103,7 @@ SC_MAX_NODES = 256
 SC_MAX_LEVELS = 16
 SC_LEDGER_KEYS = 8  # info["sc_episode"] categories (supplychain_env.py:416-417)
 SC_LEDGER_NAMES = ("stock", "stock_pen", "supply", "process", "process_pen", "ship", "ship_pen", "unmet_dem")
-SC_KERNEL_AUTO, SC_KERNEL_LANE, SC_KERNEL_LEVEL = 0, 1, 2
+SC_KERNEL_AUTO, SC_KERNEL_LANE, SC_KERNEL_LEVEL, SC_KERNEL_STAGED = 0, 1, 2, 3
 SC_LAYOUT_ENV_FASTEST, SC_LAYOUT_ENV_MAJOR = 0, 1
 SCG_STREAM_SC_DEMAND = 2
 SCG_STREAM_SC_LEADTIME = 3
@@ -124,6 +124,8 @@ class ScNode(ctypes.Structure):
         ("init_amount", (ctypes.c_int32 * SC_MAX_INIT) * SC_MAX_PRODUCTS),
         ("dests", ctypes.c_int32 * SC_MAX_DESTS), ("ship_capacity", ctypes.c_int32 * SC_MAX_DESTS),
         ("dest_costs", (ctypes.c_int32 * SC_MAX_DESTS) * SC_MAX_PRODUCTS),
+        ("in_deg", ctypes.c_int32), ("in_base", ctypes.c_int32),
+        ("in_slot", ctypes.c_int32 * SC_MAX_DESTS), ("in_stride", ctypes.c_int32 * SC_MAX_DESTS),
     ]
 
 
@@ -150,8 +152,8 @@ class ScState(ctypes.Structure):
     _fields_ = [("n_envs", ctypes.c_int64), ("env_offset", ctypes.c_int64), ("seed", ctypes.c_uint64),
                 ("episode", ctypes.c_uint32), ("time_step", ctypes.c_int32)] + [
         (f, ctypes.c_void_p) for f in ("stock", "heap_tk", "heap_val", "heap_size", "episode_return",
-                                       "final_return", "error_flags", "ledger", "ledger_kind", "final_ledger",
-                                       "final_ledger_kind")]
+                                       "final_return", "error_flags", "inbox_tk", "inbox_val", "ledger",
+                                       "ledger_kind", "final_ledger", "final_ledger_kind")]
 
 
 # Every symbol include/scgpu.h declares, with its ctypes signature.

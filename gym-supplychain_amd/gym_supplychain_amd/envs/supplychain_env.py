@@ -218,8 +218,9 @@ class SupplyChainVecEnv:
     demand_table / leadtime_table: optional device int32 tensors [N, T+1, R, P] /
     [N, T, n_lt] used for every episode instead of the Philox draws (e.g. to replay the
     reference's RandomState episodes exactly).
-    kernel: "auto" / "lane" (one lane walks one env's whole chain) or "level" (a lane
-    group per env, one lane per node of a level). Both give the same
+    kernel: "auto" / "lane" (one lane walks one env's whole chain), "level" (a lane group
+    per env, one lane per node of a level) or "staged" (one lane per env, the current
+    node's heaps in LDS, shipments through an HBM inbox); DESIGN.md §6. All give the same
     results; the state layout follows the kernel.
     spec.build_info: every step's info holds 'sc_episode' = {'rewards': [N], 'costs':
     {key: [N, P]}, 'units': {key: [N, P]}} (device views, float64; the NumPy type of every
@@ -228,7 +229,8 @@ class SupplyChainVecEnv:
     Lane kernel only.
     """
 
-    _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL}
+    _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL,
+                "staged": nat.SC_KERNEL_STAGED}
 
     def __init__(self, n_envs, nodes_info=None, spec=None, seed=0, device=None, env_offset=0, auto_reset=True,
                  obs_dtype=torch.float32, track_returns=True, demand_table=None, leadtime_table=None, kernel="auto",
@@ -275,7 +277,7 @@ class SupplyChainVecEnv:
         if spec.build_info and c.kernel == nat.SC_KERNEL_LEVEL:
             raise ValueError("build_info ledgers are kept by the lane kernel (kernel='lane' or 'auto')")
         nat.check(nat.lib.scg_sc_prepare(ctypes.byref(c), host_nodes))
-        self.kernel = "level" if c.kernel == nat.SC_KERNEL_LEVEL else "lane"
+        self.kernel = {nat.SC_KERNEL_LEVEL: "level", nat.SC_KERNEL_STAGED: "staged"}.get(c.kernel, "lane")
         self._env_major = c.layout == nat.SC_LAYOUT_ENV_MAJOR
         if (c.n_actions, c.n_obs, c.n_leadtimes) != (spec.n_actions, spec.n_obs, spec.n_leadtimes):
             raise RuntimeError("host/library disagree on the chain's action/observation sizes")
@@ -316,6 +318,10 @@ class SupplyChainVecEnv:
             self._heap_val = torch.zeros((NP, H, n_envs), dtype=torch.float64, device=dev)
             self._heap_size = torch.zeros((NP, n_envs), dtype=torch.int32, device=dev)
         self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._inbox_tk = self._inbox_val = None
+        if self.kernel == "staged":  # shipments in flight within a step [inbox_size][N]
+            self._inbox_tk = torch.zeros((max(c.inbox_size, 1), n_envs), dtype=torch.int32, device=dev)
+            self._inbox_val = torch.zeros((max(c.inbox_size, 1), n_envs), dtype=torch.float64, device=dev)
         self._ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None
         self._final_ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None
         self._obs = torch.zeros((n_envs, c.n_obs), dtype=obs_dtype, device=dev)
@@ -328,6 +334,8 @@ class SupplyChainVecEnv:
         s.episode, s.time_step = 0, -1
         s.stock, s.heap_tk, s.heap_val = self._stock.data_ptr(), self._heap_tk.data_ptr(), self._heap_val.data_ptr()
         s.heap_size, s.error_flags = self._heap_size.data_ptr(), self._err.data_ptr()
+        if self._inbox_tk is not None:
+            s.inbox_tk, s.inbox_val = self._inbox_tk.data_ptr(), self._inbox_val.data_ptr()
         s.episode_return = self._ret.data_ptr() if track_returns else None
         s.final_return = self._final_ret.data_ptr() if track_returns else None
         self.build_info = spec.build_info

@@ -223,6 +223,8 @@ SCG_API int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, 
 #define SCG_SC_KERNEL_AUTO 0
 #define SCG_SC_KERNEL_LANE 1  /* one lane walks one env's whole chain; env-fastest state       */
 #define SCG_SC_KERNEL_LEVEL 2 /* a lane group per env, one lane per node of a level; env-major */
+#define SCG_SC_KERNEL_STAGED 3 /* one lane per env, one node's heaps in LDS at a time, shipments
+                                  through a per-env global inbox; env-fastest                 */
 #define SCG_SC_LAYOUT_ENV_FASTEST 0 /* stock [NP][N], heaps [NP][H][N], sizes [NP][N]          */
 #define SCG_SC_LAYOUT_ENV_MAJOR 1   /* stock [N][NP], heaps [N][NP][H], sizes [N][NP]          */
 #define SCG_STREAM_SC_DEMAND 2u
@@ -252,6 +254,13 @@ typedef struct scg_sc_node {
   int32_t dests[SCG_SC_MAX_DESTS];             /* node indices                            */
   int32_t ship_capacity[SCG_SC_MAX_DESTS];
   int32_t dest_costs[SCG_SC_MAX_PRODUCTS][SCG_SC_MAX_DESTS];
+  /* out of scg_sc_prepare (staged kernel): this node's shipment inbox — one entry per
+   * (product, source node) at in_base + p * in_deg + k, sources k in node order — and, per
+   * destination d, where this node's shipment lands in the destination's inbox:
+   * in_slot[d] + p * in_stride[d]. */
+  int32_t in_deg, in_base;
+  int32_t in_slot[SCG_SC_MAX_DESTS];
+  int32_t in_stride[SCG_SC_MAX_DESTS];
 } scg_sc_node;
 
 typedef struct scg_sc_config {
@@ -319,6 +328,8 @@ typedef struct scg_sc_state {
   double* episode_return;       /* [N] optional                                             */
   double* final_return;         /* [N] optional: return at the terminal step                */
   int32_t* error_flags;         /* [1] DEVICE, sticky: bit 0 = a heap exceeded capacity    */
+  int32_t* inbox_tk;            /* [inbox_size][N] staged kernel: shipment time<<3|kind, -1 = none */
+  double* inbox_val;            /* [inbox_size][N] staged kernel: shipment amount               */
   /* build_info ledgers, info['sc_episode'] (:684-695, :750-760): optional, lane kernel only.
      Entry ((part * SCG_SC_LEDGER_KEYS + key) * P + p), part 0 = costs, 1 = units, keys in
      the reference's order (stock, stock_pen, supply, process, process_pen, ship, ship_pen,
@@ -335,7 +346,7 @@ SCG_API int scg_sc_struct_sizes(size_t* node_size, size_t* config_size, size_t* 
 
 /* Validate cfg against the host copy of the node table; fills n_actions, n_obs,
  * n_leadtimes, heap_capacity and max_dests. Host only. */
-SCG_API int scg_sc_prepare(scg_sc_config* cfg, const scg_sc_node* host_nodes);
+SCG_API int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* host_nodes);
 
 /* reset() for all envs (:630-682). obs: DEVICE [N][n_obs] (float32 or float64) or NULL. */
 SCG_API int scg_sc_reset(const scg_sc_config* cfg, scg_sc_state* st, void* obs, void* stream);

@@ -8,6 +8,7 @@
 
 #include "scg_supplychain_core.h"
 #include "scg_supplychain_level.h"
+#include "scg_supplychain_staged.h"
 
 namespace {
 // The level kernel's schedule on the host: a phase runs the lane body for every lane of
@@ -21,7 +22,7 @@ struct HostSched {
 };
 }  // namespace
 
-static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
                         uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
                         double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
                         int32_t* heap_size, double* ledger = nullptr, int32_t* ledger_kind = nullptr) {
@@ -86,7 +87,36 @@ static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node*
       et.led_stride = 1;
     }
     const float* a = actions + static_cast<int64_t>(t - 1) * c.A;
-    if (level) {  // sc_level_kernel's phases, lanes in turn
+    if (mode == 2) {  // sc_step_staged_kernel: one node's heaps staged, shipments via the inbox
+      std::vector<int32_t> ltk(c.P * c.H), lsz(c.P), inbox_tk(cfg->inbox_size > 0 ? cfg->inbox_size : 1, 0x7fffffff);
+      std::vector<double> lval(c.P * c.H), inbox_val(inbox_tk.size(), -1.0);
+      scg::ScEnv loc = et;
+      loc.tk = ltk.data();
+      loc.val = lval.data();
+      loc.size = lsz.data();
+      loc.hstride = 1;
+      const scg::StagedInbox in{inbox_tk.data(), inbox_val.data(), 1};
+      double* row = obs + static_cast<int64_t>(t) * c.O;
+      auto out = [row](int o, double v) { row[o] = v; };
+      double r = 0.0;
+      switch (scg::sc_maxd_bucket(cfg->max_dests)) {
+        case 2: r = scg::sc_staged_step<2>(c, et, loc, in, a, t, out); break;
+        case 4: r = scg::sc_staged_step<4>(c, et, loc, in, a, t, out); break;
+        case 8: r = scg::sc_staged_step<8>(c, et, loc, in, a, t, out); break;
+        case 16: r = scg::sc_staged_step<16>(c, et, loc, in, a, t, out); break;
+        default: r = scg::sc_staged_step<32>(c, et, loc, in, a, t, out); break;
+      }
+      rewards[t - 1] = r;
+      for (int k = 0; k < c.R * c.P; ++k) scg::sc_observe_demand(c, et, t, k, out);
+      scg::sc_observe_tail(c, t, out);
+      if (ledger) {
+        std::memcpy(ledger + static_cast<int64_t>(t - 1) * LQ, led_v.data(), sizeof(double) * LQ);
+        std::memcpy(ledger_kind + static_cast<int64_t>(t - 1) * LQ, led_k.data(), sizeof(int32_t) * LQ);
+      }
+      if (et.overflow) return 1;
+      continue;
+    }
+    if (mode == 1) {  // sc_level_kernel's phases, lanes in turn
       scg::ScLevels lv;
       lv.n = cfg->n_levels;
       for (int l = 0; l <= SCG_SC_MAX_LEVELS; ++l) lv.start[l] = cfg->level_start[l];
@@ -132,15 +162,23 @@ static int episode_impl(bool level, const scg_sc_config* cfg, const scg_sc_node*
 extern "C" int sch_episode(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr, uint64_t seed,
                            uint32_t env_id, uint32_t episode, int32_t steps, const float* actions, double* obs,
                            double* rewards, double* stock, int32_t* heap_tk, double* heap_val, int32_t* heap_size) {
-  return episode_impl(false, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+  return episode_impl(0, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
                       heap_val, heap_size);
+}
+
+extern "C" int sch_episode_staged(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                                  uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps,
+                                  const float* actions, double* obs, double* rewards, double* stock, int32_t* heap_tk,
+                                  double* heap_val, int32_t* heap_size, double* ledger, int32_t* ledger_kind) {
+  return episode_impl(2, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+                      heap_val, heap_size, ledger, ledger_kind);
 }
 
 extern "C" int sch_episode_level(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
                                  uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
                                  double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
                                  int32_t* heap_size) {
-  return episode_impl(true, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+  return episode_impl(1, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
                       heap_val, heap_size);
 }
 
@@ -148,6 +186,6 @@ extern "C" int sch_episode_ledger(const scg_sc_config* cfg, const scg_sc_node* n
                                   uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps,
                                   const float* actions, double* obs, double* rewards, double* stock, int32_t* heap_tk,
                                   double* heap_val, int32_t* heap_size, double* ledger, int32_t* ledger_kind) {
-  return episode_impl(false, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+  return episode_impl(0, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
                       heap_val, heap_size, ledger, ledger_kind);
 }

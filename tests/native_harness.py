@@ -25,10 +25,11 @@ def build():
     lib.sch_episode.restype = ctypes.c_int
     lib.sch_episode_level.restype = ctypes.c_int
     lib.sch_episode_ledger.restype = ctypes.c_int
+    lib.sch_episode_staged.restype = ctypes.c_int
     return lib
 
 
-def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=False, ledger=False):
+def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=False, ledger=False, staged=False):
     """Reset + len(actions) steps of one env; returns obs [T+1, O], rewards [T],
     stock [T+1, NP], heaps (tk, val, size) per snapshot; with ledger=True also the
     build_info ledger after every step (values [T, 2, 8, P], kinds [T, 2, 8, P])."""
@@ -46,10 +47,11 @@ def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=F
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     args = [ctypes.byref(cfg), nodes, p(thr), ctypes.c_uint64(seed), ctypes.c_uint32(env_id),
             ctypes.c_uint32(episode), ctypes.c_int32(T), p(acts), p(obs), p(rew), p(stock), p(tk), p(val), p(size)]
-    if ledger:
+    if ledger or staged:
         led_v = np.zeros((T, 2, 8, cfg.n_products))
         led_k = np.zeros((T, 2, 8, cfg.n_products), dtype=np.int32)
-        rc = lib.sch_episode_ledger(*args, p(led_v), p(led_k))
+        fn = lib.sch_episode_staged if staged else lib.sch_episode_ledger
+        rc = fn(*args, p(led_v), p(led_k))
         return rc, obs, rew, stock, (tk, val, size), (led_v, led_k)
     fn = lib.sch_episode_level if level else lib.sch_episode
     rc = fn(*args)

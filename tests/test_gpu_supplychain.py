@@ -12,7 +12,7 @@ from oracle.supplychain import SupplyChainOracle
 pytestmark = pytest.mark.gpu
 CASES = sc_cases()
 DEV = "cuda"
-KERNELS = ["lane", "level"]  # one lane per env / a lane group per env
+KERNELS = ["lane", "level", "staged"]
 
 
 def _vec(meta, n, **kw):
@@ -224,12 +224,13 @@ def test_level_kernel_equals_lane_kernel(scenario, kw):
     T = envs[0].spec.total_time_steps
     for t in range(2 * T):
         a = torch.rand((N, envs[0].n_actions), generator=gen, device=DEV) * 2.4 - 1.2
-        (o0, r0, d0, i0), (o1, r1, d1, i1) = (e.step(a) for e in envs)
-        assert torch.equal(o0, o1) and torch.equal(r0, r1) and torch.equal(d0, d1), t
-        assert torch.equal(envs[0].stock, envs[1].stock), t
-        if i0:
-            assert torch.equal(i0["terminal_observation"], i1["terminal_observation"])
-            assert torch.equal(i0["episode_return"], i1["episode_return"])
+        (o0, r0, d0, i0), *rest = (e.step(a) for e in envs)
+        for e, (o1, r1, d1, i1) in zip(envs[1:], rest):
+            assert torch.equal(o0, o1) and torch.equal(r0, r1) and torch.equal(d0, d1), (t, e.kernel)
+            assert torch.equal(envs[0].stock, e.stock), (t, e.kernel)
+            if i0:
+                assert torch.equal(i0["terminal_observation"], i1["terminal_observation"])
+                assert torch.equal(i0["episode_return"], i1["episode_return"])
     for e in envs:
         e.check_errors()
 

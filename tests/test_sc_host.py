@@ -99,3 +99,32 @@ def test_host_build_ledgers_match_reference(harness, name):
         assert np.array_equal(led_k[:, 0], g["led_cost_k"][:, n]), name
         assert np.array_equal(led_k[:, 1], g["led_units_k"][:, n]), name
         assert np.allclose(np.cumsum(rew), g["led_rewards"][:, n], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_host_build_of_staged_kernel_matches_reference(harness, name):
+    """sc_step_staged_kernel's body (scg_supplychain_staged.h): one node's heaps staged at a
+    time, shipments through the inbox — observations, rewards, stocks, heap storage order
+    and ledgers against the reference, exactly."""
+    import native_harness
+    from gym_supplychain_amd import _native as nat
+    g = load_sc(name)
+    meta = g["meta"]
+    spec, c, nodes, thr = _setup(g, nat.SC_KERNEL_STAGED)
+    assert c.kernel == nat.SC_KERNEL_STAGED and c.inbox_size > 0
+    P = spec.P
+    for n in range(g["obs"].shape[1]):
+        rc, obs, rew, stock, (tk, val, size), (led_v, led_k) = native_harness.run_episode(
+            harness, c, nodes, thr, meta["seed"], n, 0, g["actions"][:, n], staged=True)
+        assert rc == 0
+        assert np.array_equal(obs, g["obs"][:, n]), name
+        assert np.array_equal(rew, g["reward"][:, n]), name
+        assert np.array_equal(stock.reshape(stock.shape[0], -1, P), g["stock"][:, n])
+        gt = g["heap_t"][:, n].reshape(len(obs), -1, g["heap_t"].shape[-1])
+        gv = g["heap_v"][:, n].reshape(gt.shape)
+        for s_ in range(len(obs)):
+            for hp in range(gt.shape[1]):
+                k = int(size[s_, hp])
+                assert (tk[s_, hp, :k] >> 3).tolist() == gt[s_, hp, :k].tolist()
+                assert val[s_, hp, :k].tolist() == gv[s_, hp, :k].tolist()
+        assert np.array_equal(led_v[:, 0], g["led_cost"][:, n]) and np.array_equal(led_k[:, 1], g["led_units_k"][:, n])

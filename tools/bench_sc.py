@@ -113,7 +113,8 @@ def run(name, steps, warmup, n_envs, cpu, kernel="auto"):
                        "n_actions": env.n_actions, "n_obs": env.n_obs, "heap_capacity": env.heap_capacity},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "scg::sc_level_kernel" if env.kernel == "level" else "scg::sc_step(_lds)_kernel",
+                         "kernel": {"level": "scg::sc_level_kernel", "staged": "scg::sc_step_staged_kernel"}.get(
+                             env.kernel, "scg::sc_step(_lds)_kernel"),
                          "avg_kernel_us": kern_s * 1e6, "bytes_per_env_step": bpe}}
     del env, pool
     torch.cuda.empty_cache()
@@ -129,9 +130,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "both"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "staged", "all", "both"])
     a = ap.parse_args()
-    kernels = ["lane", "level"] if a.kernel == "both" else [a.kernel]
+    kernels = ["lane", "level", "staged"] if a.kernel in ("all", "both") else [a.kernel]
     for name in (["2perstage", "ntom"] if a.scenario == "both" else [a.scenario]):
         for k in kernels:
             run(name, a.steps, a.warmup, a.envs, not a.no_cpu_baseline and k == kernels[-1], k)
