@@ -208,8 +208,8 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
   }
 }
 
-// Node-staged step (scg_supplychain_staged.h): one lane per env; the heaps of the node being
-// processed are staged in LDS ([product][slot][lane], lane fastest: conflict free), the
+// Node-staged step (scg_supplychain_staged.h): one lane per env; the heap being worked on
+// is staged in LDS ([slot][lane], lane fastest: conflict free), the
 // shipments go through the env's HBM inbox, the node's observation is written while its
 // heaps are staged. No block-wide barrier: every lane only touches its own LDS column.
 template <int MAXD>
@@ -219,16 +219,10 @@ __global__ __launch_bounds__(kScBlock) void sc_step_staged_kernel(const ScArgs a
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + lane;
   if (n >= a.n) return;
   const ScCtx& c = a.c;
-  const int slots = c.P * c.H;
   double* lval = reinterpret_cast<double*>(smem);
-  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
-  int32_t* lsize = ltk + static_cast<int64_t>(slots) * kScBlock;
+  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(c.H) * kScBlock);
   ScEnv g = env_view(a, n, a.episode);
-  ScEnv loc = g;
-  loc.tk = ltk + lane;
-  loc.val = lval + lane;
-  loc.size = lsize + lane;
-  loc.hstride = kScBlock;
+  const HeapView lh{ltk + lane, lval + lane, kScBlock};
   const StagedInbox in{a.inbox_tk + n, a.inbox_val + n, a.n};
   const bool terminal = a.flags & 1;
   const bool autoreset = a.flags & 2;
@@ -241,7 +235,7 @@ __global__ __launch_bounds__(kScBlock) void sc_step_staged_kernel(const ScArgs a
     if (node_obs) main(o, x);
     if (both) extra(o, x);
   };
-  const double reward = sc_staged_step<MAXD>(c, g, loc, in, a.act + n * c.A, a.t, sink);
+  const double reward = sc_staged_step<MAXD>(c, g, lh, in, a.act + n * c.A, a.t, sink);
   a.rew[n] = reward;
   if (a.ep_ret) {
     const double r = a.ep_ret[n] + reward;
@@ -530,9 +524,9 @@ size_t sc_lds_bytes(const scg_sc_config* cfg) {
   const size_t NP = static_cast<size_t>(cfg->n_nodes) * cfg->n_products;
   return kScBlock * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
 }
-// Staged kernel: one node's heaps per lane.
+// Staged kernel: one heap per lane.
 size_t sc_staged_lds_bytes(const scg_sc_config* cfg) {
-  return kScBlock * static_cast<size_t>(cfg->n_products) * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
+  return kScBlock * static_cast<size_t>(cfg->heap_capacity) * 12;
 }
 
 // The staged kernel's inbox (scg_supplychain_staged.h): every shipment must go to a later
@@ -666,9 +660,9 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   cfg->n_obs = n_ret * P + NN * P + NN * P * cfg->avg_leadtime + 1;
   cfg->heap_capacity = H;
   cfg->max_dests = maxd;
-  // kernel: the lane kernel unless the level-parallel one is asked for (it is the slower
-  // of the two on the reference's chains as measured on MI355X)
-  const int want = cfg->kernel;
+  // kernel: as asked, the level-parallel one only when asked for (it is the slowest on the
+  // reference's chains as measured on MI355X)
+  int want = cfg->kernel;
   if (want != SCG_SC_KERNEL_AUTO && want != SCG_SC_KERNEL_LANE && want != SCG_SC_KERNEL_LEVEL &&
       want != SCG_SC_KERNEL_STAGED)
     return fail(SCG_ERR_INVALID, "kernel=%d is not a SCG_SC_KERNEL_* value", want);
@@ -676,6 +670,13 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   cfg->group = 1;
   cfg->inbox_size = 0;
   cfg->level_staged = 0;
+  // auto: the lane kernel with every heap in LDS when a block's heaps fit, else the
+  // node-staged kernel when the chain qualifies (measured faster than the lane kernel on
+  // HBM heaps), else the lane kernel on HBM heaps
+  if (want == SCG_SC_KERNEL_AUTO && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
+    std::vector<scg_sc_node> probe(nodes, nodes + NN);
+    if (sc_inbox_layout(cfg, probe.data()) >= 0) want = SCG_SC_KERNEL_STAGED;
+  }
   if (want == SCG_SC_KERNEL_STAGED) {
     const int entries = sc_inbox_layout(cfg, nodes);
     if (entries < 0)

@@ -310,22 +310,31 @@ __host__ __device__ __forceinline__ Num sc_action(const float* raw, int k) {
   return Num{static_cast<double>((raw[k] + 1.0f) / 2.0f), NK_F32};
 }
 
+// receive (:220-228) for one heap: pop every entry due now, summed in a float64 array
+__host__ __device__ __forceinline__ double sc_receive(const HeapView& h, int32_t& sz, int t) {
+  double recv = 0.0;
+  while (sz > 0 && h.time_at(0) == t) recv = recv + py_heappop(h, sz).v;
+  return recv;
+}
+
 // SC_Node.act (:208-396) for node `ni` at time t; `act` = this env's raw float32 action
 // row. Returns the node's cost with its NumPy kind. MAXD bounds the node's destinations.
-template <int MAXD, class Push = DirectPush>
+// kHeapsDone: the caller already did this node's heap work — the receive pops with their
+// stock update and the SUPPLY pushes (sc_staged_heap) — so act touches no heap of its own;
+// a node's heaps are independent of everything else act computes, so only the order of
+// operations on each heap has to be the reference's, and it is.
+template <int MAXD, class Push = DirectPush, bool kHeapsDone = false>
 __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& ltc, WordCache& dmc, int ni,
                                            const float* act, int t, const Push& push = Push()) {
   const scg_sc_node& nd = c.nodes[ni];
   const int P = c.P;
   Num cost = pyint(0);
   int lt_i = 0;
-  // receive (:220-228): pop every entry due now, summed in a float64 array
-  for (int p = 0; p < P; ++p) {
-    const HeapView h = sc_heap(c, e, ni, p);
-    int32_t& sz = sc_size(c, e, ni, p);
-    double recv = 0.0;
-    while (sz > 0 && h.time_at(0) == t) recv = recv + py_heappop(h, sz).v;
-    sc_stock(c, e, ni, p) = sc_stock(c, e, ni, p) + recv;
+  if constexpr (!kHeapsDone) {
+    for (int p = 0; p < P; ++p) {
+      int32_t& sz = sc_size(c, e, ni, p);
+      sc_stock(c, e, ni, p) = sc_stock(c, e, ni, p) + sc_receive(sc_heap(c, e, ni, p), sz, t);
+    }
   }
   // over stock capacity: penalty, excess discarded (:232-240)
   for (int p = 0; p < P; ++p) {
@@ -347,7 +356,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
       const Num cst = np_mul(amount, pyint(nd.supply_cost[p]));
       ++a_i;
       if (np_lt(pyint(0), amount)) {
-        sc_push(c, e, ni, p, t + node_leadtime(c, e, ltc, nd, t, lt_i), amount);
+        if constexpr (!kHeapsDone) sc_push(c, e, ni, p, t + node_leadtime(c, e, ltc, nd, t, lt_i), amount);
         ++lt_i;  // the lead-time cursor moves only when something was supplied (:252-254)
       }
       cost = np_add(cost, cst);
@@ -482,17 +491,22 @@ __host__ __device__ inline void sc_observe_demand(const ScCtx& c, const ScEnv& e
   out(k, sc_obs_norm(static_cast<double>(sc_demand(c, e, dmc, t, k / c.P, p) - c.dlo[p]) / range));
 }
 
-// node i, product p: stock share, then avg_leadtime in-transit bins
+// node i, product p: stock share (:433)
 template <class Sink>
-__host__ __device__ inline void sc_observe_heap(const ScCtx& c, const ScEnv& e, int t, int i, int p, Sink& out) {
+__host__ __device__ __forceinline__ void sc_observe_stock(const ScCtx& c, const ScEnv& e, int i, int p, Sink& out) {
+  const int base = c.R * c.P + i * (c.P + c.P * c.avg_lt);
+  out(base + p, sc_obs_norm(sc_stock(c, e, i, p) / static_cast<double>(c.nodes[i].stock_capacity[p])));
+}
+
+// node i, product p: avg_leadtime in-transit bins over heap h of size sz (:445-461)
+template <class Sink>
+__host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& h, int32_t sz, int t, int i, int p,
+                                                Sink& out) {
   const scg_sc_node& nd = c.nodes[i];
   const int nb = c.avg_lt;
   const int base = c.R * c.P + i * (c.P + c.P * nb);
-  out(base + p, sc_obs_norm(sc_stock(c, e, i, p) / static_cast<double>(nd.stock_capacity[p])));
   int o = base + c.P + p * nb;
   const int first = t + 1, last = t + c.avg_lt;
-  const HeapView h = sc_heap(c, e, i, p);
-  const int32_t sz = sc_size(c, e, i, p);
   if (sz == 0) {
     for (int b = first; b <= last; ++b) out(o++, sc_obs_norm(0.0));
     return;
@@ -514,6 +528,13 @@ __host__ __device__ inline void sc_observe_heap(const ScCtx& c, const ScEnv& e, 
     ++k;
   }
   out(o, sc_obs_norm(np_div(bin, pyint(nd.max_ship[p] * (c.max_lt - (last - first)))).v));
+}
+
+// node i, product p: stock share, then avg_leadtime in-transit bins
+template <class Sink>
+__host__ __device__ inline void sc_observe_heap(const ScCtx& c, const ScEnv& e, int t, int i, int p, Sink& out) {
+  sc_observe_stock(c, e, i, p, out);
+  sc_observe_bins(c, sc_heap(c, e, i, p), sc_size(c, e, i, p), t, i, p, out);
 }
 
 template <class Sink>

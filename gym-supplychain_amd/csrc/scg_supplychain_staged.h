@@ -7,14 +7,17 @@
 // pays a chain of dependent global loads for every heap operation (a push sifts through
 // up to log2(H) parents); here, per node in order:
 //
-//   stage    node i's heaps (P x H entries) from HBM into fast memory (LDS on the device)
-//   drain    the shipments earlier nodes made to i this step, from i's inbox, in source
-//            order — the order in which the reference pushed them — with heappush
-//   act      SC_Node.act (:208-396) on the staged heaps; i's own shipments are written to
-//            the inbox entries of its destinations (plain stores, one per destination and
-//            product, -1 when nothing is shipped) instead of being pushed
-//   observe  i's stock share and in-transit bins (:428-463) — its heaps are final
-//   store    the heaps back to HBM
+//   per product p, heap (i, p) alone (H entries, so the LDS a lane needs is one heap):
+//     stage    the heap from HBM into fast memory (LDS on the device)
+//     drain    the shipments earlier nodes made to (i, p) this step, from i's inbox, in
+//              source order — the order in which the reference pushed them — with heappush
+//     receive  the pops due now and the stock update (:220-228)
+//     supply   the SUPPLY push (:243-259) — the heap's last operation of the step
+//     observe  its in-transit bins (:445-461), then store it back to HBM
+//   act      the rest of SC_Node.act (:208-396), touching no heap of i; i's own shipments
+//            are written to the inbox entries of its destinations (plain stores, one per
+//            destination and product, -1 when nothing is shipped) instead of being pushed
+//   observe  i's stock shares
 //
 // Heap storage order, float rounding and the lead-time cursor are the reference's (the
 // pushes into a heap happen in the same order, before the same pops). The inbox is a
@@ -47,44 +50,61 @@ struct StagedInbox {
   }
 };
 
-// Copy node i's heaps (live entries) and sizes between two env views.
-__host__ __device__ inline void sc_copy_node_heaps(const ScCtx& c, const ScEnv& from, ScEnv& to, int i) {
-  for (int p = 0; p < c.P; ++p) {
-    const int32_t sz = sc_size(c, from, i, p);
-    sc_size(c, to, i, p) = sz;
-    const HeapView a = sc_heap(c, from, i, p), b = sc_heap(c, to, i, p);
-    for (int j = 0; j < sz; ++j) b.put(j, a.get(j));
+// Everything node i does to heap (i, p) in step t, on a copy staged in `lh` (one heap,
+// H entries): the drain of the shipments earlier nodes made to it, in source order (:347);
+// the receive pops and the stock update (:220-228); the SUPPLY push (:243-259, the
+// lead-time cursor `lt_i` and supply-action index `a_i` advanced as act advances them);
+// then, the heap being final for the step, its in-transit bins (:445-461). Heap storage
+// order is the reference's: the same pushes and pops happen in the same order.
+template <class Sink>
+__host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
+                                               WordCache& ltc, const float* act, int t, int i, int p, int& a_i,
+                                               int& lt_i, Sink& out) {
+  const scg_sc_node& nd = c.nodes[i];
+  const HeapView gh = sc_heap(c, g, i, p);
+  int32_t& gsz = sc_size(c, g, i, p);
+  int32_t sz = gsz;
+  for (int j = 0; j < sz; ++j) lh.put(j, gh.get(j));
+  for (int k = 0; k < nd.in_deg; ++k) {
+    const int64_t q = nd.in_base + static_cast<int64_t>(p) * nd.in_deg + k;
+    const int32_t tk = in.tk[q * in.stride];
+    if (tk >= 0 && !py_heappush(lh, sz, c.H, HeapEntry{tk, in.val[q * in.stride]})) g.overflow = 1;
   }
+  double& st = sc_stock(c, g, i, p);
+  st = st + sc_receive(lh, sz, t);
+  if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) {
+    const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));
+    ++a_i;
+    if (np_lt(pyint(0), amount)) {
+      const HeapEntry e{he_pack(t + node_leadtime(c, g, ltc, nd, t, lt_i), amount.k), amount.v};
+      if (!py_heappush(lh, sz, c.H, e)) g.overflow = 1;
+      ++lt_i;
+    }
+  }
+  sc_observe_bins(c, lh, sz, t, i, p, out);
+  for (int j = 0; j < sz; ++j) gh.put(j, lh.get(j));
+  gsz = sz;
 }
 
 // SupplyChainEnv.step body (:704-738) plus the node part of _build_observation (:762-791)
-// for time t. `g` views the env's state in HBM; `loc` views the same env with heap arrays
-// that hold one node's heaps (its hnode0 is set per node). out(o, x) receives the node
-// observation elements (the caller adds the demand and time-to-go ones). Returns the reward.
+// for time t. `g` views the env's state in HBM; `lh` is the one-heap staging area. Per
+// node in order: its heaps one product at a time (sc_staged_heap), then act on everything
+// else (no heap access: kHeapsDone), its shipments going to the inbox, then its stock
+// shares. out(o, x) receives the node observation elements (the caller adds the demand and
+// time-to-go ones). Returns the reward.
 template <int MAXD, class Sink>
-__host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, ScEnv& loc, const StagedInbox& in,
+__host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
                                                  const float* act, int t, Sink& out) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   Num total = pyint(0);
   for (int i = 0; i < c.n_nodes; ++i) {
     const scg_sc_node& nd = c.nodes[i];
-    loc.hnode0 = i;
-    sc_copy_node_heaps(c, g, loc, i);
-    for (int p = 0; p < c.P; ++p) {  // the shipments of earlier nodes, in their order (:347)
-      int32_t& sz = sc_size(c, loc, i, p);
-      const HeapView h = sc_heap(c, loc, i, p);
-      for (int k = 0; k < nd.in_deg; ++k) {
-        const int64_t q = nd.in_base + static_cast<int64_t>(p) * nd.in_deg + k;
-        const int32_t tk = in.tk[q * in.stride];
-        if (tk >= 0 && !py_heappush(h, sz, c.H, HeapEntry{tk, in.val[q * in.stride]})) loc.overflow = 1;
-      }
-    }
+    int a_i = 0, lt_i = 0;
+    for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out);
     if (!nd.last_level) in.clear(c, i);
-    total = np_add(total, sc_node_act<MAXD, StagedInbox>(c, loc, ltc, dmc, i, act, t, in));
-    for (int p = 0; p < c.P; ++p) sc_observe_heap(c, loc, t, i, p, out);
-    sc_copy_node_heaps(c, loc, g, i);
+    total = np_add(total, sc_node_act<MAXD, StagedInbox, true>(c, g, ltc, dmc, i, act, t, in));
+    for (int p = 0; p < c.P; ++p) sc_observe_stock(c, g, i, p, out);
   }
-  g.overflow |= loc.overflow;
   return np_neg(total).v;
 }
 

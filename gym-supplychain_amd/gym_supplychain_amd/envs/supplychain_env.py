@@ -11,14 +11,13 @@ device buffers.
 
 Differences from the reference:
   * per-episode demand and stochastic lead times are drawn on device with Philox (same
-    distributions: uniform randint demand, clip(1 + Poisson(avg-1), 1, max) lead times)
-    instead of MT19937 RandomState, keyed by `seed` and the global env id;
+    distributions: uniform / normal / sinusoidal demand per product (envs/demand.py),
+    clip(1 + Poisson(avg-1), 1, max) lead times) instead of MT19937 RandomState, keyed by
+    `seed` and the global env id; caller tables replay any host draw exactly;
   * actions are float32 (the declared Box dtype); the vec env's observations are float32
     by default (float64, the reference's dtype, on request and in the single-env class);
-  * normal / sinusoidal demand and demand_config_by_product are not yet supported and
-    raise NotImplementedError;
-  * build_info=True keeps info['sc_episode'] on the device (lane kernel); the drop-in env
-    returns it with the reference's per-entry NumPy types.
+  * build_info=True keeps info['sc_episode'] on the device (lane and staged kernels); the
+    drop-in env returns it with the reference's per-entry NumPy types.
 """
 import ctypes
 import os
@@ -226,7 +225,7 @@ class SupplyChainVecEnv:
     {key: [N, P]}, 'units': {key: [N, P]}} (device views, float64; the NumPy type of every
     entry in ledger_kinds()), the reference's episode ledgers (:684-695, :750-760); with
     auto-reset the terminal step adds 'terminal_sc_episode' for the finished episode.
-    Lane kernel only.
+    Lane and staged kernels.
     """
 
     _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL,
@@ -275,7 +274,7 @@ class SupplyChainVecEnv:
             raise ValueError(f"kernel must be one of {sorted(self._KERNELS)}, got {kernel!r}")
         c.kernel = self._KERNELS[kernel]
         if spec.build_info and c.kernel == nat.SC_KERNEL_LEVEL:
-            raise ValueError("build_info ledgers are kept by the lane kernel (kernel='lane' or 'auto')")
+            raise ValueError("build_info ledgers are kept by the lane and staged kernels (kernel='lane', 'staged' or 'auto')")
         nat.check(nat.lib.scg_sc_prepare(ctypes.byref(c), host_nodes))
         self.kernel = {nat.SC_KERNEL_LEVEL: "level", nat.SC_KERNEL_STAGED: "staged"}.get(c.kernel, "lane")
         self._env_major = c.layout == nat.SC_LAYOUT_ENV_MAJOR

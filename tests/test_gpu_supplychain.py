@@ -235,16 +235,18 @@ def test_level_kernel_equals_lane_kernel(scenario, kw):
         e.check_errors()
 
 
+@pytest.mark.parametrize("kernel", ["lane", "staged"])
 @pytest.mark.parametrize("name", CASES)
-def test_ledgers_match_reference(name):
+def test_ledgers_match_reference(name, kernel):
     """build_info: info['sc_episode'] on the device against the reference's ledgers after
-    every step — values and NumPy types of every cost/unit entry, exactly."""
+    every step — values and NumPy types of every cost/unit entry, exactly (both kernels
+    that keep ledgers)."""
     from gym_supplychain_amd import _native as nat
     g = load_sc(name)
     meta = g["meta"]
     T, N = meta["T"], g["obs"].shape[1]
-    env = _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, build_info=True)
-    assert env.kernel == "lane"
+    env = _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, build_info=True, kernel=kernel)
+    assert env.kernel == kernel
     env.reset()
     acts = torch.as_tensor(g["actions"], device=DEV)
     for t in range(T):

@@ -128,3 +128,13 @@ def test_host_build_of_staged_kernel_matches_reference(harness, name):
                 assert (tk[s_, hp, :k] >> 3).tolist() == gt[s_, hp, :k].tolist()
                 assert val[s_, hp, :k].tolist() == gv[s_, hp, :k].tolist()
         assert np.array_equal(led_v[:, 0], g["led_cost"][:, n]) and np.array_equal(led_k[:, 1], g["led_units_k"][:, n])
+
+
+def test_auto_kernel_choice():
+    """kernel='auto' (scg_sc_prepare, host only): the lane kernel with every heap in LDS when
+    a block's heaps fit (2-per-stage), the node-staged kernel on the wide ntom chain."""
+    from gym_supplychain_amd import _native as nat
+    _, c, _, _ = _setup(load_sc("2perstage"), nat.SC_KERNEL_AUTO)
+    assert c.kernel == nat.SC_KERNEL_LANE and c.inbox_size == 0
+    _, c, _, _ = _setup(load_sc("ntom"), nat.SC_KERNEL_AUTO)
+    assert c.kernel == nat.SC_KERNEL_STAGED and c.inbox_size > 0
