@@ -498,10 +498,15 @@ __host__ __device__ __forceinline__ void sc_observe_stock(const ScCtx& c, const 
   out(base + p, sc_obs_norm(sc_stock(c, e, i, p) / static_cast<double>(c.nodes[i].stock_capacity[p])));
 }
 
-// node i, product p: avg_leadtime in-transit bins over heap h of size sz (:445-461)
-template <class Sink>
+struct NoVisit {
+  __host__ __device__ __forceinline__ void operator()(int, const HeapEntry&) const {}
+};
+
+// node i, product p: avg_leadtime in-transit bins over heap h of size sz (:445-461). The
+// walk reads every entry once, in storage order; visit(k, entry) sees each of them.
+template <class Sink, class Visit = NoVisit>
 __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& h, int32_t sz, int t, int i, int p,
-                                                Sink& out) {
+                                                Sink& out, const Visit& visit = Visit()) {
   const scg_sc_node& nd = c.nodes[i];
   const int nb = c.avg_lt;
   const int base = c.R * c.P + i * (c.P + c.P * nb);
@@ -516,6 +521,7 @@ __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& 
     Num bin = pyint(0);
     while (k < sz && h.time_at(k) == when) {
       const HeapEntry en = h.get(k);
+      visit(k, en);
       bin = np_add(bin, Num{en.v, he_kind(en.tk)});
       ++k;
     }
@@ -524,6 +530,7 @@ __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& 
   Num bin = pyint(0);
   while (k < sz) {
     const HeapEntry en = h.get(k);
+    visit(k, en);
     bin = np_add(bin, Num{en.v, he_kind(en.tk)});
     ++k;
   }

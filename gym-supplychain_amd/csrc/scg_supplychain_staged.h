@@ -63,15 +63,40 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
   const scg_sc_node& nd = c.nodes[i];
   const HeapView gh = sc_heap(c, g, i, p);
   int32_t& gsz = sc_size(c, g, i, p);
-  int32_t sz = gsz;
-  for (int j = 0; j < sz; ++j) lh.put(j, gh.get(j));
-  for (int k = 0; k < nd.in_deg; ++k) {
-    const int64_t q = nd.in_base + static_cast<int64_t>(p) * nd.in_deg + k;
-    const int32_t tk = in.tk[q * in.stride];
-    if (tk >= 0 && !py_heappush(lh, sz, c.H, HeapEntry{tk, in.val[q * in.stride]})) g.overflow = 1;
-  }
   double& st = sc_stock(c, g, i, p);
-  st = st + sc_receive(lh, sz, t);
+  const double st0 = st;
+  // Global loads go out kChunk at a time (all issued before the first is used), so a heap
+  // copy or an inbox drain waits on memory once per chunk instead of once per entry; the
+  // heap size, the stock and the first inbox chunk are requested together up front.
+  // (kChunk = 8 pushed the kernel to 256 VGPRs, one wave per SIMD, and ran slower.)
+  constexpr int kChunk = 4;
+  const int64_t q0 = nd.in_base + static_cast<int64_t>(p) * nd.in_deg;
+  HeapEntry ib[kChunk];
+#pragma unroll
+  for (int u = 0; u < kChunk; ++u)
+    if (u < nd.in_deg) ib[u] = HeapEntry{in.tk[(q0 + u) * in.stride], in.val[(q0 + u) * in.stride]};
+  int32_t sz = gsz;
+  for (int j0 = 0; j0 < sz; j0 += kChunk) {
+    HeapEntry b[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u)
+      if (j0 + u < sz) b[u] = gh.get(j0 + u);
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u)
+      if (j0 + u < sz) lh.put(j0 + u, b[u]);
+  }
+  for (int k0 = 0; k0 < nd.in_deg; k0 += kChunk) {
+    if (k0 > 0) {
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u)
+        if (k0 + u < nd.in_deg)
+          ib[u] = HeapEntry{in.tk[(q0 + k0 + u) * in.stride], in.val[(q0 + k0 + u) * in.stride]};
+    }
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u)  // in source order (:347)
+      if (k0 + u < nd.in_deg && ib[u].tk >= 0 && !py_heappush(lh, sz, c.H, ib[u])) g.overflow = 1;
+  }
+  st = st0 + sc_receive(lh, sz, t);
   if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) {
     const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));
     ++a_i;
@@ -81,8 +106,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
       ++lt_i;
     }
   }
-  sc_observe_bins(c, lh, sz, t, i, p, out);
-  for (int j = 0; j < sz; ++j) gh.put(j, lh.get(j));
+  sc_observe_bins(c, lh, sz, t, i, p, out, [&](int k, const HeapEntry& e) { gh.put(k, e); });  // copy back
   gsz = sz;
 }
 
@@ -91,7 +115,8 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 // node in order: its heaps one product at a time (sc_staged_heap), then act on everything
 // else (no heap access: kHeapsDone), its shipments going to the inbox, then its stock
 // shares. out(o, x) receives the node observation elements (the caller adds the demand and
-// time-to-go ones). Returns the reward.
+// time-to-go ones). Returns the reward. (Staging the node's stocks in LDS as well measured
+// no faster on MI355X: stock accesses are few and cache-resident.)
 template <int MAXD, class Sink>
 __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
                                                  const float* act, int t, Sink& out) {
