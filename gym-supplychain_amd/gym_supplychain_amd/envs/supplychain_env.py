@@ -444,6 +444,20 @@ class SupplyChainVecEnv:
                          for j, key in enumerate(nat.SC_LEDGER_NAMES)}
         return out
 
+    @property
+    def kernel_symbol(self):
+        """The step kernel scg_sc_step launches for this batch, as rocprofv3 names it (the
+        lane kernel keeps every heap in LDS when a block's share fits 64 KiB)."""
+        c = self._cfg
+        d = c.max_dests
+        maxd = 2 if d <= 2 else 4 if d <= 4 else 8 if d <= 8 else 16 if d <= 16 else 32
+        if self.kernel == "level":
+            return f"scg::sc_level_kernel<{maxd}, {'true' if c.level_staged else 'false'}>"
+        if self.kernel == "staged":
+            return f"scg::sc_step_staged_kernel<{maxd}>"
+        lds = 64 * len(self.spec.nodes) * self.spec.P * (12 * c.heap_capacity + 4)
+        return f"scg::sc_step_lds_kernel<{maxd}>" if lds <= 64 * 1024 else f"scg::sc_step_kernel<{maxd}>"
+
     def check_errors(self):
         """Raise if any env's in-transit heap overflowed its capacity (never expected: the
         capacity is the chain's provable bound, scg_sc_prepare)."""

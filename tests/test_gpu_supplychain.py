@@ -331,3 +331,15 @@ def test_drop_in_env_build_info():
         assert np.isclose(led["rewards"], total)
         assert np.isclose(total, -sum(float(x) for k in led["costs"] for x in led["costs"][k]))
     assert done
+
+
+def test_auto_kernel_symbols():
+    """kernel='auto' on the bench configs: the lane kernel with heaps in LDS (config 3), the
+    node-staged kernel (config 4); kernel_symbol names what rocprofv3 reports."""
+    import gym_supplychain_amd as gsa
+    env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV)
+    assert env.kernel == "lane" and env.kernel_symbol == "scg::sc_step_lds_kernel<2>"
+    env = gsa.make_vec("sc-Nperstage-multiproduct-v0", 64, device=DEV, nodes_per_echelon=[8, 8, 8, 16])
+    assert env.kernel == "staged" and env.kernel_symbol == "scg::sc_step_staged_kernel<16>"
+    env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, kernel="level")
+    assert env.kernel_symbol.startswith("scg::sc_level_kernel<2, ")

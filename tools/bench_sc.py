@@ -77,6 +77,25 @@ def cpu_baseline(name, budget=1.5, max_procs=16):
                       f"oracle.supplychain.SupplyChainOracle; {steps} env-steps"}
 
 
+def pmc_traffic(symbol, n_envs, name):
+    """HBM bytes per launch of `symbol` from the latest committed PMC summary
+    (profiles/rNN_pmc_summary.json: tools/gpu_pmc.sh runs this tool at the default sizes with
+    the auto kernel; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM). None when absent or
+    for another batch size."""
+    import glob
+    if n_envs != SCENARIOS[name]["n_envs"]:
+        return None, None
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        traffic = json.load(f).get("traffic", {})
+    for k, t in traffic.items():
+        if symbol.split("::")[-1] in k and t.get("hbm_bytes_per_launch"):
+            return t["hbm_bytes_per_launch"], os.path.relpath(files[-1], REPO)
+    return None, None
+
+
 def run(name, steps, warmup, n_envs, cpu, kernel="auto"):
     import torch
     import gym_supplychain_amd as gsa
@@ -104,6 +123,7 @@ def run(name, steps, warmup, n_envs, cpu, kernel="auto"):
     kern_s = sum(s.elapsed_time(e) for s, e in ev) / 1e3 / steps
     bpe = sc["bytes_per_env_step"]
     achieved = bpe * N / kern_s / 1e9
+    traffic, traffic_src = pmc_traffic(env.kernel_symbol, N, name)
     line = {"metric": f"env-steps/sec, {sc['env_id']} {sc['kwargs'] or ''} x{N} envs on 1 MI355X",
             "value": N * steps / wall, "unit": "env-steps/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
             "ms_per_step": wall * 1e3 / steps, "higher_is_better": True, "dtype": "f32 actions/obs, f64 state",
@@ -112,9 +132,8 @@ def run(name, steps, warmup, n_envs, cpu, kernel="auto"):
                        "kernel": env.kernel,
                        "n_actions": env.n_actions, "n_obs": env.n_obs, "heap_capacity": env.heap_capacity},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": {"level": "scg::sc_level_kernel", "staged": "scg::sc_step_staged_kernel"}.get(
-                             env.kernel, "scg::sc_step(_lds)_kernel"),
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": bpe * N, "kernel": env.kernel_symbol,
                          "avg_kernel_us": kern_s * 1e6, "bytes_per_env_step": bpe}}
     del env, pool
     torch.cuda.empty_cache()
