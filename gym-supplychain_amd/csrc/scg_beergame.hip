@@ -126,6 +126,35 @@ __device__ __forceinline__ int32_t poisson_invert(const BgArgs& a, uint32_t u) {
   return x;
 }
 
+// Poisson thresholds held one per lane (entry k in lane k % 64 of t0 for k < 64, else of
+// t1): one coalesced vector load per wave ahead of use, then the count #{k : thr[k] <= u}
+// broadcasts each entry with readlane (exec-independent) instead of a scalar-indexed loop
+// that waits on memory every iteration. The loading lanes must all be active at the load
+// (the kernels load before their tail lanes return). on = false: use poisson_invert.
+struct LaneThresholds {
+  uint32_t t0, t1;
+  int32_t len;
+  bool on;
+
+  __device__ __forceinline__ static LaneThresholds load(const BgArgs& a) {
+    LaneThresholds r{0u, 0u, a.pthr_len, a.demand_mode == SCG_DEMAND_POISSON && a.pthr_len <= 128};
+    if (r.on) {
+      const int li = threadIdx.x & 63;
+      if (li < r.len) r.t0 = a.pthr[li];
+      if (64 + li < r.len) r.t1 = a.pthr[64 + li];
+    }
+    return r;
+  }
+  __device__ __forceinline__ int32_t count_le(uint32_t u) const {
+    int32_t x = 0;
+    const int32_t n0 = len < 64 ? len : 64;
+    for (int k = 0; k < n0; ++k) x += (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t0), k)) <= u) ? 1 : 0;
+    for (int k = 64; k < len; ++k)
+      x += (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t1), k - 64)) <= u) ? 1 : 0;
+    return x;
+  }
+};
+
 // Customer demand of env n for `week` (1-based): beergame_env.py:79 reads
 // customer_demand[week-1]; here per env from a table (TABLE) or drawn on device
 // (POISSON, UNIFORM). The shared FIXED list arrives as a per-week kernel argument instead.
@@ -442,10 +471,15 @@ struct RingLds {
 // the action row in and the obs/reward (and history) rows out touch HBM. With LDS the
 // pipeline ring is staged in shared memory for the whole launch (loaded once, stored
 // once); otherwise its rows are read-modify-written through L2.
+// Weeks run in groups of kRolloutGroup: the group's action rows are all requested before
+// its first week, so a launch waits on memory once per group instead of once per week.
+constexpr int kRolloutGroup = 8;
+
 template <int L, class Ring>
 __device__ __forceinline__ void rollout_body(const BgArgs& a, int64_t n, int32_t K, const RolloutWeeks& weeks,
                                              const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
-                                             int32_t* __restrict__ rew_out, const Ring& ring) {
+                                             int32_t* __restrict__ rew_out, const Ring& ring,
+                                             const LaneThresholds& pt) {
   const int64_t row = n * L;
   const int64_t stride = a.n * L;
   int32_t inv[L], bk[L], op[L], iacc[L], bacc[L];
@@ -458,13 +492,28 @@ __device__ __forceinline__ void rollout_body(const BgArgs& a, int64_t n, int32_t
   if (a.bk_acc) load_row<L>(a.bk_acc + row, bacc);
   int64_t ret = a.ep_ret ? a.ep_ret[n] : 0;
   uint32_t episode = a.episode;
-  for (int32_t k = 0; k < K; ++k) {
+  for (int32_t k0 = 0; k0 < K; k0 += kRolloutGroup) {
+  int32_t group_act[kRolloutGroup][L];
+#pragma unroll
+  for (int u = 0; u < kRolloutGroup; ++u)
+    if (k0 + u < K) load_row<L>(acts + (k0 + u) * stride + row, group_act[u]);
+#pragma unroll
+  for (int u = 0; u < kRolloutGroup; ++u) {
+    const int32_t k = k0 + u;
+    if (k >= K) break;
     const WeekInfo wk = weeks.wk[k];
-    int32_t act[L], due[L], obs[L], ic[L], bc[L], ship[L];
-    load_row<L>(acts + k * stride + row, act);
+    int32_t due[L], obs[L], ic[L], bc[L], ship[L];
+    int32_t(&act)[L] = group_act[u];
     zero_row<L>(due);
     if (wk.read_slot >= 0) ring.load(wk.read_slot, due);
-    const int32_t demand = a.demand_mode == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand(a, n, wk.week, episode);
+    int32_t demand;
+    if (a.demand_mode == SCG_DEMAND_FIXED)
+      demand = wk.demand_fixed;
+    else if (pt.on)
+      demand = pt.count_le(scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), episode,
+                                            static_cast<uint32_t>(wk.week - 1), SCG_STREAM_DEMAND));
+    else
+      demand = week_demand(a, n, wk.week, episode);
     const int32_t reward = step_core<L>(a.h, a.b, demand, wk.mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
     if (wk.mode == MODE_STORE) {
       ring.store(wk.write_slot, ship);
@@ -503,6 +552,7 @@ __device__ __forceinline__ void rollout_body(const BgArgs& a, int64_t n, int32_t
     if (obs_out) store_row<L>(obs_out + k * stride + row, obs);
     if (rew_out) rew_out[k * a.n + n] = reward;
   }
+  }
   store_row<L>(a.inv + row, inv);
   store_row<L>(a.bk + row, bk);
   store_row<L>(a.op + row, op);
@@ -516,8 +566,9 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int3
                                                             const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
                                                             int32_t* __restrict__ rew_out) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const LaneThresholds pt = LaneThresholds::load(a);  // every lane still active
   if (n >= a.n) return;
-  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, RingHbm<L>{a.ring, a.n * L, n * L});
+  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, RingHbm<L>{a.ring, a.n * L, n * L}, pt);
 }
 
 template <int L>
@@ -527,6 +578,7 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_lds_kernel(const BgArgs a, 
                                                                 int32_t* __restrict__ rew_out) {
   extern __shared__ int32_t lds_ring[];
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const LaneThresholds pt = LaneThresholds::load(a);  // every lane still active
   if (n >= a.n) return;  // lanes only touch their own LDS column: no block barrier needed
   const RingHbm<L> hbm{a.ring, a.n * L, n * L};
   const RingLds<L> lds{lds_ring + threadIdx.x};
@@ -535,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_lds_kernel(const BgArgs a, 
     hbm.load(s, v);
     lds.store(s, v);
   }
-  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, lds);
+  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, lds, pt);
   for (int s = 0; s < a.ring_slots; ++s) {
     int32_t v[L];
     lds.load(s, v);
