@@ -58,7 +58,10 @@ def build_library(debug=False, verbose=True):
             print(f"[build_native] {OUT} up to date")
         return OUT
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-fvisibility=hidden", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function",
+           "-fvisibility=hidden", "-ffp-contract=off",
+           # leading scalar kernel arguments preloaded into SGPRs at wave launch (gfx950);
+           # kernels whose first argument is a struct are unaffected
+           "-mllvm", "-amdgpu-kernarg-preload-count=7", "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function",
            "-I", os.path.join(REPO, "include"), "-I", CSRC,
            "-O1" if debug else "-O3", "-o", OUT + ".tmp"] + srcs
     if verbose:

@@ -266,52 +266,81 @@ __device__ __forceinline__ void zero_row(int32_t (&v)[L]) {
   for (int l = 0; l < L; ++l) v[l] = 0;
 }
 
+// Week plan packed into one dword for the step kernel's preloaded arguments:
+// bits 0-7 read_slot + 1 (0: nothing due), 8-15 write_slot, 16-17 mode, 18-19 flags.
+inline uint32_t pack_week(const WeekInfo& wk) {
+  return static_cast<uint32_t>(wk.read_slot + 1) | (static_cast<uint32_t>(wk.write_slot) << 8) |
+         (static_cast<uint32_t>(wk.mode) << 16) | (static_cast<uint32_t>(wk.flags) << 18);
+}
+
 // step(action) for one env per lane: every row this launch reads is loaded up front (one
 // round of memory latency), the week is computed in registers, then every row is stored.
+// The leading scalar arguments (the four state rows' and the ring's base pointers, the env
+// count and the packed week plan: 12 dwords) are preloaded into SGPRs at wave launch
+// (gfx950 kernarg preload, build flag -amdgpu-kernarg-preload-count), so the first row
+// loads issue without waiting on the kernarg segment; the rest of the arguments arrive
+// through scalar loads that overlap those rows.
 template <int L, int DM>
-__global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const WeekInfo wk) {
-  // Every kernel argument the week reads, requested at once: the kernarg segment is cold
-  // in the scalar cache at every launch, and loads the compiler would otherwise sink into
-  // the branches below each cost one more dependent scalar round trip before the first
-  // row load can issue.
-  asm volatile("" ::"s"(a.n), "s"(a.inv), "s"(a.bk), "s"(a.op), "s"(a.act), "s"(a.ring), "s"(a.inv_acc),
-               "s"(a.bk_acc), "s"(a.ep_ret), "s"(a.final_ret), "s"(a.rew), "s"(a.hist), "s"(a.term_obs), "s"(a.obs),
-               "s"(a.h), "s"(a.b));
-  asm volatile("" ::"s"(wk.week), "s"(wk.read_slot), "s"(wk.write_slot), "s"(wk.mode), "s"(wk.flags),
-               "s"(wk.demand_fixed), "s"(a.demand_mode), "s"(a.pthr), "s"(a.pthr_len), "s"(a.key0), "s"(a.key1),
-               "s"(a.episode), "s"(a.env_offset), "s"(a.demand_table), "s"(a.demand_lo), "s"(a.demand_hi));
+__global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ inv_p, int32_t* __restrict__ bk_p,
+                                                         int32_t* __restrict__ op_p, const int32_t* __restrict__ act_p,
+                                                         int32_t* __restrict__ ring_p, uint32_t n32, uint32_t wpack,
+                                                         const BgArgs a, const WeekInfo wk) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (n >= a.n) return;
+  const int32_t read_slot = static_cast<int32_t>(wpack & 0xffu) - 1;
+  const int32_t write_slot = static_cast<int32_t>((wpack >> 8) & 0xffu);
+  const int32_t mode = static_cast<int32_t>((wpack >> 16) & 3u);
+  const bool terminal = wpack & (1u << 18);
+  const bool autoreset = wpack & (2u << 18);
   const int64_t row = n * L;
-  const int64_t stride = a.n * L;
-  const bool terminal = wk.flags & 1;
-  const bool autoreset = wk.flags & 2;
+  const int64_t stride = static_cast<int64_t>(n32) * L;
+  const bool live = n < static_cast<int64_t>(n32);
 
   int32_t inv[L], bk[L], op[L], act[L], due[L], cur[L], iacc[L], bacc[L];
-  load_row<L>(a.inv + row, inv);
-  load_row<L>(a.bk + row, bk);
-  load_row<L>(a.op + row, op);
-  load_row<L>(a.act + row, act);
   zero_row<L>(due);
   zero_row<L>(cur);
+  if (live) {
+    load_row<L>(inv_p + row, inv);
+    load_row<L>(bk_p + row, bk);
+    load_row<L>(op_p + row, op);
+    load_row<L>(act_p + row, act);
+    if (read_slot >= 0) load_row<L>(ring_p + read_slot * stride + row, due);
+    if (mode == MODE_ADD) load_row<L>(ring_p + write_slot * stride + row, cur);
+  }
+  // Every other kernel argument the week reads, requested at once (one scalar round trip
+  // instead of one per branch the compiler would sink them into).
+  asm volatile("" ::"s"(a.inv_acc), "s"(a.bk_acc), "s"(a.ep_ret), "s"(a.final_ret), "s"(a.rew), "s"(a.hist),
+               "s"(a.term_obs), "s"(a.obs), "s"(a.h), "s"(a.b), "s"(wk.week), "s"(wk.demand_fixed));
+  asm volatile("" ::"s"(a.pthr), "s"(a.pthr_len), "s"(a.key0), "s"(a.key1), "s"(a.episode), "s"(a.env_offset),
+               "s"(a.demand_table), "s"(a.demand_lo), "s"(a.demand_hi));
+  // Poisson thresholds one per lane, loaded while every lane of the wave is still active.
+  LaneThresholds thr{};
+  if constexpr (DM == SCG_DEMAND_POISSON) thr = LaneThresholds::load(a);
+  if (!live) return;
   zero_row<L>(iacc);
   zero_row<L>(bacc);
-  if (wk.read_slot >= 0) load_row<L>(a.ring + wk.read_slot * stride + row, due);
-  if (wk.mode == MODE_ADD) load_row<L>(a.ring + wk.write_slot * stride + row, cur);
   if (!autoreset && a.inv_acc) load_row<L>(a.inv_acc + row, iacc);
   if (!autoreset && a.bk_acc) load_row<L>(a.bk_acc + row, bacc);
   const int64_t ret0 = a.ep_ret ? a.ep_ret[n] : 0;
-  const int32_t demand = DM == SCG_DEMAND_FIXED ? wk.demand_fixed : week_demand<DM>(a, n, wk.week, a.episode);
+  int32_t demand;
+  if constexpr (DM == SCG_DEMAND_FIXED) {
+    demand = wk.demand_fixed;
+  } else if constexpr (DM == SCG_DEMAND_POISSON) {
+    const uint32_t u = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), a.episode,
+                                        static_cast<uint32_t>(wk.week - 1), SCG_STREAM_DEMAND);
+    demand = thr.on ? thr.count_le(u) : poisson_invert(a, u);
+  } else {
+    demand = week_demand<DM>(a, n, wk.week, a.episode);
+  }
 
   int32_t ship[L], obs[L], ic[L], bc[L];
-  const int32_t reward = step_core<L>(a.h, a.b, demand, wk.mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
+  const int32_t reward = step_core<L>(a.h, a.b, demand, mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
 
-  if (wk.mode == MODE_STORE) {
-    store_row<L>(a.ring + wk.write_slot * stride + row, ship);
-  } else if (wk.mode == MODE_ADD) {
+  if (mode == MODE_STORE) {
+    store_row<L>(ring_p + write_slot * stride + row, ship);
+  } else if (mode == MODE_ADD) {
 #pragma unroll
     for (int l = 0; l < L; ++l) cur[l] += ship[l];
-    store_row<L>(a.ring + wk.write_slot * stride + row, cur);
+    store_row<L>(ring_p + write_slot * stride + row, cur);
   }  // MODE_DROP: arrives after the horizon, never observable
   a.rew[n] = reward;
   if (a.hist) store_row<L>(a.hist + static_cast<int64_t>(wk.week) * stride + row, op);  // :123
@@ -322,9 +351,9 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(const BgArgs a, const W
     reset_env<L>(a, n, a.obs);
     return;
   }
-  store_row<L>(a.inv + row, inv);
-  store_row<L>(a.bk + row, bk);
-  store_row<L>(a.op + row, op);
+  store_row<L>(inv_p + row, inv);
+  store_row<L>(bk_p + row, bk);
+  store_row<L>(op_p + row, op);
   store_row<L>(a.obs + row, obs);
   if (a.inv_acc) {  // :131
 #pragma unroll
@@ -653,7 +682,7 @@ template <int DM>
 int launch_step_dm(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk, hipEvent_t ev0,
                    hipEvent_t ev1) {
   switch (L) {
-#define X(l) case l: hipExtLaunchKernelGGL(HIP_KERNEL_NAME(bg_step_kernel<l, DM>), grid, dim3(kBlock), 0, s, ev0, ev1, 0, a, wk); break;
+#define X(l) case l: hipExtLaunchKernelGGL(HIP_KERNEL_NAME(bg_step_kernel<l, DM>), grid, dim3(kBlock), 0, s, ev0, ev1, 0, a.inv, a.bk, a.op, a.act, a.ring, static_cast<uint32_t>(a.n), pack_week(wk), a, wk); break;
     SCG_LEVEL_CASES(X)
 #undef X
     default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
@@ -698,6 +727,7 @@ int check_state(const scg_bg_config* cfg, const scg_bg_state* st) {
   if (!cfg || !st) return fail(SCG_ERR_INVALID, "null config/state");
   if (!cfg->plan || cfg->ring_slots <= 0) return fail(SCG_ERR_INVALID, "config not prepared (call scg_bg_prepare)");
   if (st->n_envs <= 0) return fail(SCG_ERR_INVALID, "n_envs must be > 0");
+  if (st->n_envs > INT32_MAX) return fail(SCG_ERR_INVALID, "n_envs must be <= %d per shard", INT32_MAX);
   if (st->env_offset < 0 || st->env_offset + st->n_envs > (int64_t(1) << 32))
     return fail(SCG_ERR_INVALID, "global env ids must fit in 32 bits");
   if (!st->inventory || !st->backlog || !st->orders_placed || !st->shipments)
