@@ -5,7 +5,8 @@
 // them, :714-736); the per-env body is scg_supplychain_core.h. State arrays are
 // env-fastest ([slot][N]) so lanes touching the same node/heap slot read one contiguous
 // row; heap positions are data-dependent, so heap traffic is row-gathered through L2.
-// The chain description (scg_sc_node[]) is wave-uniform and read with scalar loads.
+// The chain description (scg_sc_node[]) is wave-uniform and read with scalar loads (constant
+// address space, ScNode in scg_supplychain_core.h).
 
 #include <hip/hip_runtime.h>
 
@@ -415,8 +416,8 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   ScArgs a;
   std::memset(&a, 0, sizeof(a));
   ScCtx& c = a.c;
-  c.nodes = cfg->nodes;
-  c.lt_thr = cfg->leadtime_poisson;
+  c.nodes = const_tab(cfg->nodes);
+  c.lt_thr = const_tab(cfg->leadtime_poisson);
   c.dem_tab = cfg->demand_table;
   c.lt_tab = cfg->leadtime_table;
   c.n_nodes = cfg->n_nodes;

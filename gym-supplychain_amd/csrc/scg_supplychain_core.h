@@ -21,10 +21,29 @@ namespace scg {
 // Compile-time destination bound used for a chain whose widest node ships to d nodes.
 __host__ __device__ constexpr int sc_maxd_bucket(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32; }
 
+// Launch-uniform configuration tables (node records, threshold and sinusoid tables) are
+// read through the constant address space on the device: a wave-uniform index into one
+// becomes a scalar load through the scalar cache, which the compiler batches, instead of
+// a vector load that waits on vmcnt before every use (each node field the step reads
+// was one such round trip). No kernel writes these tables, so the non-coherent scalar
+// cache is safe. On the host the qualifier is empty.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SCG_CONST_AS __attribute__((address_space(4)))
+#else
+#define SCG_CONST_AS
+#endif
+using ScNode = const SCG_CONST_AS scg_sc_node;
+template <class T>
+using ConstTab = const SCG_CONST_AS T*;
+template <class T>
+__host__ __device__ __forceinline__ ConstTab<T> const_tab(const T* p) {
+  return (ConstTab<T>)p;
+}
+
 // Launch-uniform view of the configuration.
 struct ScCtx {
-  const scg_sc_node* nodes;
-  const uint32_t* lt_thr;
+  ScNode* nodes;
+  ConstTab<uint32_t> lt_thr;
   const int32_t* dem_tab;  // [N][T+1][R][P] or null (Philox)
   const int32_t* lt_tab;   // [N][T][n_lt] or null (Philox)
   int32_t n_nodes, P, R, A, O, H, T;
@@ -35,8 +54,8 @@ struct ScCtx {
   int32_t dkind[SCG_SC_MAX_PRODUCTS], dlo[SCG_SC_MAX_PRODUCTS], dhi[SCG_SC_MAX_PRODUCTS];
   int32_t dpert_lo[SCG_SC_MAX_PRODUCTS], dpert_n[SCG_SC_MAX_PRODUCTS];
   int64_t doff[SCG_SC_MAX_PRODUCTS];
-  const uint32_t* dthr;
-  const double* dbase;
+  ConstTab<uint32_t> dthr;
+  ConstTab<double> dbase;
 };
 
 // The demand models of a config: per product, or every product uniform on
@@ -51,8 +70,8 @@ inline void sc_ctx_demand(ScCtx& c, const scg_sc_config* cfg) {
     c.dpert_n[p] = m ? cfg->demand_pert_n[p] : 0;
     c.doff[p] = m ? cfg->demand_off[p] : 0;
   }
-  c.dthr = cfg->demand_thr;
-  c.dbase = cfg->demand_base;
+  c.dthr = const_tab(cfg->demand_thr);
+  c.dbase = const_tab(cfg->demand_base);
 }
 
 // One env's state: element i of a per-env array lives at [i * stride] (stock) or
@@ -139,7 +158,7 @@ __host__ __device__ __forceinline__ uint32_t cached_word(const ScCtx& c, const S
 }
 
 // #{k < n : thr[k] <= u} over a nondecreasing table (upper bound)
-__host__ __device__ __forceinline__ int32_t sc_count_le(const uint32_t* thr, int32_t n, uint32_t u) {
+__host__ __device__ __forceinline__ int32_t sc_count_le(ConstTab<uint32_t> thr, int32_t n, uint32_t u) {
   int32_t a = 0, b = n;
   while (a < b) {
     const int32_t m = (a + b) >> 1;
@@ -190,7 +209,7 @@ __host__ __device__ __forceinline__ int32_t sc_leadtime(const ScCtx& c, const Sc
 
 // Lead time #i of a node in step t (deterministic: avg_leadtime for every action, :724).
 __host__ __device__ __forceinline__ int32_t node_leadtime(const ScCtx& c, const ScEnv& e, WordCache& wc,
-                                                          const scg_sc_node& nd, int t, int i) {
+                                                          ScNode& nd, int t, int i) {
   if (!c.stochastic) return c.avg_lt;
   return sc_leadtime(c, e, wc, t, nd.leadtime_offset + i);
 }
@@ -217,7 +236,7 @@ struct DirectPush {
 // re-seeded at times 1..k (initial_supply entries first, then initial_shipments, each
 // pushed with heappush). Heaps are independent, so any lane may reset any of them.
 __host__ __device__ inline void sc_reset_heap(const ScCtx& c, ScEnv& e, int i, int p) {
-  const scg_sc_node& nd = c.nodes[i];
+  ScNode& nd = c.nodes[i];
   sc_stock(c, e, i, p) = static_cast<double>(nd.initial_stock[p]);
   sc_size(c, e, i, p) = 0;
   for (int j = 0; j < nd.n_init[p]; ++j) sc_push(c, e, i, p, nd.init_time[p][j], pyint(nd.init_amount[p][j]));
@@ -326,7 +345,7 @@ __host__ __device__ __forceinline__ double sc_receive(const HeapView& h, int32_t
 template <int MAXD, class Push = DirectPush, bool kHeapsDone = false>
 __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& ltc, WordCache& dmc, int ni,
                                            const float* act, int t, const Push& push = Push()) {
-  const scg_sc_node& nd = c.nodes[ni];
+  ScNode& nd = c.nodes[ni];
   const int P = c.P;
   Num cost = pyint(0);
   int lt_i = 0;
@@ -507,7 +526,7 @@ struct NoVisit {
 template <class Sink, class Visit = NoVisit>
 __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& h, int32_t sz, int t, int i, int p,
                                                 Sink& out, const Visit& visit = Visit()) {
-  const scg_sc_node& nd = c.nodes[i];
+  ScNode& nd = c.nodes[i];
   const int nb = c.avg_lt;
   const int base = c.R * c.P + i * (c.P + c.P * nb);
   int o = base + c.P + p * nb;

@@ -37,14 +37,14 @@ struct StagedInbox {
   static constexpr bool kUnroll = true;  // a store per destination
   __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv&, int src, int d, int /*dest*/, int p,
                                                 int32_t time, Num amount) const {
-    const scg_sc_node& nd = c.nodes[src];
+    ScNode& nd = c.nodes[src];
     const int64_t q = nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d];
     tk[q * stride] = he_pack(time, amount.k);
     val[q * stride] = amount.v;
   }
   // node src ships nothing this step unless its act writes an entry
   __host__ __device__ __forceinline__ void clear(const ScCtx& c, int src) const {
-    const scg_sc_node& nd = c.nodes[src];
+    ScNode& nd = c.nodes[src];
     for (int d = 0; d < nd.n_dests; ++d)
       for (int p = 0; p < c.P; ++p) tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = -1;
   }
@@ -60,7 +60,7 @@ template <class Sink>
 __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
                                                WordCache& ltc, const float* act, int t, int i, int p, int& a_i,
                                                int& lt_i, Sink& out) {
-  const scg_sc_node& nd = c.nodes[i];
+  ScNode& nd = c.nodes[i];
   const HeapView gh = sc_heap(c, g, i, p);
   int32_t& gsz = sc_size(c, g, i, p);
   double& st = sc_stock(c, g, i, p);
@@ -123,7 +123,7 @@ __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   Num total = pyint(0);
   for (int i = 0; i < c.n_nodes; ++i) {
-    const scg_sc_node& nd = c.nodes[i];
+    ScNode& nd = c.nodes[i];
     int a_i = 0, lt_i = 0;
     for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out);
     if (!nd.last_level) in.clear(c, i);

@@ -28,8 +28,8 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
                         int32_t* heap_size, double* ledger = nullptr, int32_t* ledger_kind = nullptr) {
   scg::ScCtx c;
   std::memset(&c, 0, sizeof(c));
-  c.nodes = nodes;
-  c.lt_thr = lt_thr;
+  c.nodes = scg::const_tab(nodes);
+  c.lt_thr = scg::const_tab(lt_thr);
   c.n_nodes = cfg->n_nodes;
   c.P = cfg->n_products;
   c.R = cfg->n_retailers;
