@@ -12,14 +12,15 @@ output, resident in HBM). Envs shard across ranks by global id; the only collect
 async RCCL all-gather of per-env episode returns at each episode end.
 
 Rank 0 prints ONE JSON line. `value` is the wall clock of the timed step loop, in which no
-launch is stamped. `roofline` prices the step kernel: algorithmic bytes per launch
-(DESIGN.md §6, 260 B per env on a regular week) ÷ the kernel's average duration, taken
-after the timed region from `--kernel-samples` more launches (whole 35-week cycles), each
-stamped by hipExtLaunchKernel with its own dispatch begin/end (the interval rocprofv3
-reports) and run alone — a stamped launch queued behind another also counts the tail of
-its predecessor, and a stamped launch is slower than a plain one, so the timed loop stays
-unstamped. `gpu_timeline_us_per_launch` is the timed region's GPU time per step (events
-on the launch stream around the loop: kernels plus the boundaries between them).
+launch is stamped. `roofline` prices the step kernel: the algorithmic bytes of the timed
+region's launches (DESIGN.md §6, 260 B per env on a regular week, summed week by week) ÷
+the timed region's GPU time, from HIP events recorded on the launch stream around the
+loop — live, and an upper bound on the kernels' duration (it also holds the boundaries
+between launches), so `achieved` is conservative. Cross-check: `isolated_kernel_us`, the
+average of `--kernel-samples` further launches (whole 35-week cycles) after the timed
+region, each stamped by hipExtLaunchKernel with its own dispatch begin/end (the interval
+rocprofv3 reports) and run alone — stamping inside the loop would slow it, and a stamped
+launch queued behind another also counts the tail of its predecessor.
 `cpu_baseline` times oracle.beergame.BeerGameOracle — the per-env NumPy restatement of the
 reference step() — on the host's cores (rank 0, N = 1 only).
 """
@@ -186,6 +187,8 @@ def main():
 
     run(args.warmup)
     plan = list(env._plan)
+    w_timed = env.week  # the timed region's launches run weeks w_timed+1, w_timed+2, ... (mod 35)
+    timed_bytes = sum(week_bytes((w_timed + i) % WEEKS + 1) for i in range(args.steps))
     # timed region: plain launches, nothing stamped; GPU-timeline events on the launch stream
     # (torch's current stream, which VecEnv.step launches on) bracket it
     t_ev0, t_ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -224,8 +227,8 @@ def main():
 
     if rank == 0:
         value = N * world * args.steps / elapsed
-        avg_kernel_s = kern_ms / 1e3 / n_sampled
-        achieved = sampled_bytes / (kern_ms / 1e3) / 1e9
+        avg_kernel_s = timeline_ms / 1e3 / args.steps
+        achieved = timed_bytes / (timeline_ms / 1e3) / 1e9
         traffic, traffic_src = pmc_traffic(n_envs=N)
         line = {
             "metric": "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X",
@@ -247,8 +250,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "scg::bg_step_kernel<4, 2> (L = 4, Poisson demand)", "avg_kernel_us": avg_kernel_s * 1e6,
-                         "bytes_per_launch": sampled_bytes / n_sampled, "launches_timed": n_sampled,
-                         "gpu_timeline_us_per_launch": timeline_ms * 1e3 / args.steps},
+                         "avg_kernel_source": "HIP events on the launch stream around the timed region",
+                         "bytes_per_launch": timed_bytes / args.steps, "launches_timed": args.steps,
+                         "isolated_kernel_us": kern_ms * 1e3 / n_sampled, "isolated_launches": n_sampled,
+                         "isolated_frac": sampled_bytes / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
