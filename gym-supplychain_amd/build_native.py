@@ -49,6 +49,14 @@ def build(debug=False, verbose=True):
     return lib
 
 
+# hipcc flags of libscgpu.so (tools/exp_build.py builds its variants with the same ones)
+HIP_FLAGS = ["-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-ffp-contract=off",
+             # leading scalar kernel arguments preloaded into SGPRs at wave launch (gfx950);
+             # kernels whose first argument is a struct are unaffected
+             "-mllvm", "-amdgpu-kernarg-preload-count=7",
+             "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function"]
+
+
 def build_library(debug=False, verbose=True):
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
@@ -57,13 +65,8 @@ def build_library(debug=False, verbose=True):
         if verbose:
             print(f"[build_native] {OUT} up to date")
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-fvisibility=hidden", "-ffp-contract=off",
-           # leading scalar kernel arguments preloaded into SGPRs at wave launch (gfx950);
-           # kernels whose first argument is a struct are unaffected
-           "-mllvm", "-amdgpu-kernarg-preload-count=7", "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function",
-           "-I", os.path.join(REPO, "include"), "-I", CSRC,
-           "-O1" if debug else "-O3", "-o", OUT + ".tmp"] + srcs
+    cmd = [hipcc(), f"--offload-arch={ARCH}"] + HIP_FLAGS + [
+        "-I", os.path.join(REPO, "include"), "-I", CSRC, "-O1" if debug else "-O3", "-o", OUT + ".tmp"] + srcs
     if verbose:
         print("[build_native]", " ".join(cmd))
     subprocess.run(cmd, check=True)

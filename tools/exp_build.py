@@ -60,9 +60,8 @@ def main():
                         ignore=shutil.ignore_patterns("*.so", "__pycache__"))
     out = os.path.join(pkg, "libscgpu.so")
     srcs = [os.path.join(csrc, s) for s in build_native.SOURCES]
-    cmd = [build_native.hipcc(), f"--offload-arch={build_native.ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-fvisibility=hidden", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall",
-           "-Wno-unused-function", "-I", inc, "-I", csrc, "-O3", "-o", out] + \
+    cmd = [build_native.hipcc(), f"--offload-arch={build_native.ARCH}"] + build_native.HIP_FLAGS + \
+        ["-I", inc, "-I", csrc, "-O3", "-o", out] + \
         [f"-D{d}" for d in a.defines] + srcs
     print("[exp_build]", " ".join(cmd))
     subprocess.run(cmd, check=True)
