@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "scg_common.h"
+#include "scg_const.h"
 #include "scg_philox.h"
 #include "scgpu.h"
 
@@ -123,6 +124,20 @@ __device__ __forceinline__ int32_t poisson_invert(const BgArgs& a, uint32_t u) {
   const uint32_t* __restrict__ thr = a.pthr;
   int32_t x = 0;
   for (int k = 0; k < a.pthr_len; ++k) x += (thr[k] <= u) ? 1 : 0;
+  return x;
+}
+
+// Inverse CDF with the thresholds read through the scalar cache (constant address space),
+// eight per scalar load: the count waits on lgkmcnt only, so it runs while the step
+// kernel's row loads are still in flight instead of after them.
+__device__ __forceinline__ int32_t poisson_count_scalar(ConstTab<uint32_t> thr, int32_t len, uint32_t u) {
+  int32_t x = 0;
+  int k = 0;
+  for (; k + 8 <= len; k += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x += (thr[k + j] <= u) ? 1 : 0;
+  }
+  for (; k < len; ++k) x += (thr[k] <= u) ? 1 : 0;
   return x;
 }
 
@@ -279,7 +294,8 @@ inline uint32_t pack_week(const WeekInfo& wk) {
 // count and the packed week plan: 12 dwords) are preloaded into SGPRs at wave launch
 // (gfx950 kernarg preload, build flag -amdgpu-kernarg-preload-count), so the first row
 // loads issue without waiting on the kernarg segment; the rest of the arguments arrive
-// through scalar loads that overlap those rows.
+// through scalar loads that overlap those rows, and the Poisson inversion reads its
+// thresholds through the scalar cache, so it too runs while the rows are in flight.
 template <int L, int DM>
 __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ inv_p, int32_t* __restrict__ bk_p,
                                                          int32_t* __restrict__ op_p, const int32_t* __restrict__ act_p,
@@ -293,29 +309,20 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
   const bool autoreset = wpack & (2u << 18);
   const int64_t row = n * L;
   const int64_t stride = static_cast<int64_t>(n32) * L;
-  const bool live = n < static_cast<int64_t>(n32);
+  if (n >= static_cast<int64_t>(n32)) return;
 
   int32_t inv[L], bk[L], op[L], act[L], due[L], cur[L], iacc[L], bacc[L];
   zero_row<L>(due);
   zero_row<L>(cur);
-  if (live) {
-    load_row<L>(inv_p + row, inv);
-    load_row<L>(bk_p + row, bk);
-    load_row<L>(op_p + row, op);
-    load_row<L>(act_p + row, act);
-    if (read_slot >= 0) load_row<L>(ring_p + read_slot * stride + row, due);
-    if (mode == MODE_ADD) load_row<L>(ring_p + write_slot * stride + row, cur);
-  }
-  // Every other kernel argument the week reads, requested at once (one scalar round trip
-  // instead of one per branch the compiler would sink them into).
-  asm volatile("" ::"s"(a.inv_acc), "s"(a.bk_acc), "s"(a.ep_ret), "s"(a.final_ret), "s"(a.rew), "s"(a.hist),
-               "s"(a.term_obs), "s"(a.obs), "s"(a.h), "s"(a.b), "s"(wk.week), "s"(wk.demand_fixed));
-  asm volatile("" ::"s"(a.pthr), "s"(a.pthr_len), "s"(a.key0), "s"(a.key1), "s"(a.episode), "s"(a.env_offset),
-               "s"(a.demand_table), "s"(a.demand_lo), "s"(a.demand_hi));
-  // Poisson thresholds one per lane, loaded while every lane of the wave is still active.
-  LaneThresholds thr{};
-  if constexpr (DM == SCG_DEMAND_POISSON) thr = LaneThresholds::load(a);
-  if (!live) return;
+  load_row<L>(inv_p + row, inv);
+  load_row<L>(bk_p + row, bk);
+  load_row<L>(op_p + row, op);
+  load_row<L>(act_p + row, act);
+  if (read_slot >= 0) load_row<L>(ring_p + read_slot * stride + row, due);
+  if (mode == MODE_ADD) load_row<L>(ring_p + write_slot * stride + row, cur);
+  // The remaining arguments are left to the compiler's scalar loads: they issue after
+  // these rows and overlap them (forcing them up front made the register allocator reuse
+  // a kernarg SGPR and wait on the kernarg segment before the first row load).
   zero_row<L>(iacc);
   zero_row<L>(bacc);
   if (!autoreset && a.inv_acc) load_row<L>(a.inv_acc + row, iacc);
@@ -327,7 +334,7 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
   } else if constexpr (DM == SCG_DEMAND_POISSON) {
     const uint32_t u = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), a.episode,
                                         static_cast<uint32_t>(wk.week - 1), SCG_STREAM_DEMAND);
-    demand = thr.on ? thr.count_le(u) : poisson_invert(a, u);
+    demand = poisson_count_scalar(const_tab(a.pthr), a.pthr_len, u);
   } else {
     demand = week_demand<DM>(a, n, wk.week, a.episode);
   }

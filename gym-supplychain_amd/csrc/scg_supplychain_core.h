@@ -11,6 +11,7 @@
 
 #include <stdint.h>
 
+#include "scg_const.h"
 #include "scg_npscalar.h"
 #include "scg_philox.h"
 #include "scg_pyheap.h"
@@ -21,24 +22,9 @@ namespace scg {
 // Compile-time destination bound used for a chain whose widest node ships to d nodes.
 __host__ __device__ constexpr int sc_maxd_bucket(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32; }
 
-// Launch-uniform configuration tables (node records, threshold and sinusoid tables) are
-// read through the constant address space on the device: a wave-uniform index into one
-// becomes a scalar load through the scalar cache, which the compiler batches, instead of
-// a vector load that waits on vmcnt before every use (each node field the step reads
-// was one such round trip). No kernel writes these tables, so the non-coherent scalar
-// cache is safe. On the host the qualifier is empty.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define SCG_CONST_AS __attribute__((address_space(4)))
-#else
-#define SCG_CONST_AS
-#endif
+// Node records and threshold/sinusoid tables are read through the constant address space
+// (scg_const.h): their wave-uniform fields become batched scalar loads.
 using ScNode = const SCG_CONST_AS scg_sc_node;
-template <class T>
-using ConstTab = const SCG_CONST_AS T*;
-template <class T>
-__host__ __device__ __forceinline__ ConstTab<T> const_tab(const T* p) {
-  return (ConstTab<T>)p;
-}
 
 // Launch-uniform view of the configuration.
 struct ScCtx {

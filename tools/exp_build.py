@@ -39,7 +39,10 @@ def main():
     os.makedirs(inc)
     for f in os.listdir(os.path.join(PKG, "csrc")):
         src = os.path.join(PKG, "csrc", f)
-        text = git_show(a.rev, f"gym-supplychain_amd/csrc/{f}") if a.rev else open(src).read()
+        try:
+            text = git_show(a.rev, f"gym-supplychain_amd/csrc/{f}") if a.rev else open(src).read()
+        except subprocess.CalledProcessError:  # a file the revision does not have yet
+            continue
         open(os.path.join(csrc, f), "w").write(text)
     hdr = git_show(a.rev, "include/scgpu.h") if a.rev else open(os.path.join(REPO, "include", "scgpu.h")).read()
     open(os.path.join(inc, "scgpu.h"), "w").write(hdr)
