@@ -118,18 +118,11 @@ __device__ __forceinline__ void fill_row(int32_t* __restrict__ p, int32_t x) {
   store_row<L>(p, v);
 }
 
-// Inverse CDF on uint32 thresholds: #{k : thr[k] <= u}. The table index is wave-uniform,
-// so it streams through scalar loads; no divergent search.
-__device__ __forceinline__ int32_t poisson_invert(const BgArgs& a, uint32_t u) {
-  const uint32_t* __restrict__ thr = a.pthr;
-  int32_t x = 0;
-  for (int k = 0; k < a.pthr_len; ++k) x += (thr[k] <= u) ? 1 : 0;
-  return x;
-}
-
-// Inverse CDF with the thresholds read through the scalar cache (constant address space),
-// eight per scalar load: the count waits on lgkmcnt only, so it runs while the step
-// kernel's row loads are still in flight instead of after them.
+// Inverse CDF on uint32 thresholds, #{k : thr[k] <= u}, with the table read through the
+// scalar cache (constant address space), eight entries per scalar load: the table index is
+// wave-uniform, and the count waits on lgkmcnt only, so it runs while a kernel's row loads
+// are still in flight instead of after them (a vector load of the table waited on vmcnt,
+// i.e. for every row first).
 __device__ __forceinline__ int32_t poisson_count_scalar(ConstTab<uint32_t> thr, int32_t len, uint32_t u) {
   int32_t x = 0;
   int k = 0;
@@ -139,6 +132,10 @@ __device__ __forceinline__ int32_t poisson_count_scalar(ConstTab<uint32_t> thr, 
   }
   for (; k < len; ++k) x += (thr[k] <= u) ? 1 : 0;
   return x;
+}
+
+__device__ __forceinline__ int32_t poisson_invert(const BgArgs& a, uint32_t u) {
+  return poisson_count_scalar(const_tab(a.pthr), a.pthr_len, u);
 }
 
 // Poisson thresholds held one per lane (entry k in lane k % 64 of t0 for k < 64, else of
@@ -334,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
   } else if constexpr (DM == SCG_DEMAND_POISSON) {
     const uint32_t u = scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), a.episode,
                                         static_cast<uint32_t>(wk.week - 1), SCG_STREAM_DEMAND);
-    demand = poisson_count_scalar(const_tab(a.pthr), a.pthr_len, u);
+    demand = poisson_invert(a, u);
   } else {
     demand = week_demand<DM>(a, n, wk.week, a.episode);
   }
