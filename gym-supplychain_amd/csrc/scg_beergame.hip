@@ -138,35 +138,6 @@ __device__ __forceinline__ int32_t poisson_invert(const BgArgs& a, uint32_t u) {
   return poisson_count_scalar(const_tab(a.pthr), a.pthr_len, u);
 }
 
-// Poisson thresholds held one per lane (entry k in lane k % 64 of t0 for k < 64, else of
-// t1): one coalesced vector load per wave ahead of use, then the count #{k : thr[k] <= u}
-// broadcasts each entry with readlane (exec-independent) instead of a scalar-indexed loop
-// that waits on memory every iteration. The loading lanes must all be active at the load
-// (the kernels load before their tail lanes return). on = false: use poisson_invert.
-struct LaneThresholds {
-  uint32_t t0, t1;
-  int32_t len;
-  bool on;
-
-  __device__ __forceinline__ static LaneThresholds load(const BgArgs& a) {
-    LaneThresholds r{0u, 0u, a.pthr_len, a.demand_mode == SCG_DEMAND_POISSON && a.pthr_len <= 128};
-    if (r.on) {
-      const int li = threadIdx.x & 63;
-      if (li < r.len) r.t0 = a.pthr[li];
-      if (64 + li < r.len) r.t1 = a.pthr[64 + li];
-    }
-    return r;
-  }
-  __device__ __forceinline__ int32_t count_le(uint32_t u) const {
-    int32_t x = 0;
-    const int32_t n0 = len < 64 ? len : 64;
-    for (int k = 0; k < n0; ++k) x += (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t0), k)) <= u) ? 1 : 0;
-    for (int k = 64; k < len; ++k)
-      x += (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t1), k - 64)) <= u) ? 1 : 0;
-    return x;
-  }
-};
-
 // Customer demand of env n for `week` (1-based): beergame_env.py:79 reads
 // customer_demand[week-1]; here per env from a table (TABLE) or drawn on device
 // (POISSON, UNIFORM). The shared FIXED list arrives as a per-week kernel argument instead.
@@ -511,8 +482,7 @@ constexpr int kRolloutGroup = 8;
 template <int L, class Ring>
 __device__ __forceinline__ void rollout_body(const BgArgs& a, int64_t n, int32_t K, const RolloutWeeks& weeks,
                                              const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
-                                             int32_t* __restrict__ rew_out, const Ring& ring,
-                                             const LaneThresholds& pt) {
+                                             int32_t* __restrict__ rew_out, const Ring& ring) {
   const int64_t row = n * L;
   const int64_t stride = a.n * L;
   int32_t inv[L], bk[L], op[L], iacc[L], bacc[L];
@@ -542,9 +512,6 @@ __device__ __forceinline__ void rollout_body(const BgArgs& a, int64_t n, int32_t
     int32_t demand;
     if (a.demand_mode == SCG_DEMAND_FIXED)
       demand = wk.demand_fixed;
-    else if (pt.on)
-      demand = pt.count_le(scg::philox_word(a.key0, a.key1, static_cast<uint32_t>(a.env_offset + n), episode,
-                                            static_cast<uint32_t>(wk.week - 1), SCG_STREAM_DEMAND));
     else
       demand = week_demand(a, n, wk.week, episode);
     const int32_t reward = step_core<L>(a.h, a.b, demand, wk.mode == MODE_DIRECT, due, inv, bk, op, act, ship, obs, ic, bc);
@@ -599,9 +566,8 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_kernel(const BgArgs a, int3
                                                             const int32_t* __restrict__ acts, int32_t* __restrict__ obs_out,
                                                             int32_t* __restrict__ rew_out) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  const LaneThresholds pt = LaneThresholds::load(a);  // every lane still active
   if (n >= a.n) return;
-  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, RingHbm<L>{a.ring, a.n * L, n * L}, pt);
+  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, RingHbm<L>{a.ring, a.n * L, n * L});
 }
 
 template <int L>
@@ -611,7 +577,6 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_lds_kernel(const BgArgs a, 
                                                                 int32_t* __restrict__ rew_out) {
   extern __shared__ int32_t lds_ring[];
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  const LaneThresholds pt = LaneThresholds::load(a);  // every lane still active
   if (n >= a.n) return;  // lanes only touch their own LDS column: no block barrier needed
   const RingHbm<L> hbm{a.ring, a.n * L, n * L};
   const RingLds<L> lds{lds_ring + threadIdx.x};
@@ -620,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void bg_rollout_lds_kernel(const BgArgs a, 
     hbm.load(s, v);
     lds.store(s, v);
   }
-  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, lds, pt);
+  rollout_body<L>(a, n, K, weeks, acts, obs_out, rew_out, lds);
   for (int s = 0; s < a.ring_slots; ++s) {
     int32_t v[L];
     lds.load(s, v);
