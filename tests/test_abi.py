@@ -121,3 +121,27 @@ def test_config_mirrors_reference_defaults_and_errors():
         BeerGameConfig({"inv_cost": 1.5})
     with pytest.raises(ValueError):
         BeerGameConfig({"levels": 6})  # default initial_inventory has 4 entries
+
+
+def test_step_rejects_shards_beyond_int32_before_any_launch():
+    """The step kernel takes the shard's env count as one preloaded 32-bit argument: the
+    launcher rejects larger shards (validation runs before any HIP call, so no GPU needed)."""
+    from gym_supplychain_amd import _native as nat
+    T = 35
+    c = nat.BgConfig()
+    c.levels, c.max_weeks = 4, T
+    d = (ctypes.c_int32 * (T + 1))(*([2] * (T + 1)))
+    dem = (ctypes.c_int32 * T)(*([8] * T))
+    plan = (ctypes.c_int32 * (T + 1))()
+    c.shipment_delays = ctypes.cast(d, ctypes.c_void_p)
+    c.customer_demand = ctypes.cast(dem, ctypes.c_void_p)
+    c.plan = ctypes.cast(plan, ctypes.c_void_p)
+    assert nat.lib.scg_bg_prepare(ctypes.byref(c)) == 0
+    st = nat.BgState()
+    st.n_envs, st.env_offset, st.week = 2 ** 31, 0, 0
+    fake = ctypes.c_void_p(0x1000)  # never dereferenced: the call fails validation first
+    for f in ("inventory", "backlog", "orders_placed", "shipments"):
+        setattr(st, f, fake)
+    out = ctypes.c_int32(0)
+    rc = nat.lib.scg_bg_step(ctypes.byref(c), ctypes.byref(st), fake, fake, fake, None, 0, ctypes.byref(out), None)
+    assert rc == nat.SCG_ERR_INVALID and "n_envs" in nat.last_error()
