@@ -41,20 +41,20 @@ class EpisodeReturnGather:
         self.group = group
         self.n = int(n_per_rank)
         self.device = torch.device(device)
-        self._stage = torch.zeros(self.n, dtype=torch.int64, device=self.device)
+        self._stage = torch.zeros(self.n, dtype=torch.int64, device=self.device) if self.world > 1 else None
         self._out = torch.zeros(self.world * self.n, dtype=torch.int64, device=self.device)
         self._work = None
         self.gathers = 0
 
     def on_episode_end(self, final_return):
+        if self.world == 1:  # the snapshot is the result: one device copy per episode
+            self._out.copy_(final_return, non_blocking=True)
+            self.gathers += 1
+            return
         if self._work is not None:
             self._work.wait()  # previous gather still reading _stage
         self._stage.copy_(final_return, non_blocking=True)
-        if self.world > 1:
-            self._work = dist.all_gather_into_tensor(self._out, self._stage, group=self.group, async_op=True)
-        else:
-            self._out.copy_(self._stage, non_blocking=True)
-            self._work = None
+        self._work = dist.all_gather_into_tensor(self._out, self._stage, group=self.group, async_op=True)
         self.gathers += 1
 
     def result(self):
