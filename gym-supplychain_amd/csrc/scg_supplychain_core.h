@@ -185,11 +185,16 @@ __host__ __device__ __forceinline__ int32_t sc_demand(const ScCtx& c, const ScEn
 // leadtimes[t-1, k]: clip(1 + Poisson(avg-1), 1, max)   (:670-672)
 __host__ __device__ __forceinline__ int32_t sc_leadtime(const ScCtx& c, const ScEnv& e, WordCache& wc, int t, int k) {
   const uint32_t j = static_cast<uint32_t>((t - 1) * c.n_lt + k);
-  if (c.lt_tab) return c.lt_tab[e.local * (static_cast<int64_t>(c.T) * c.n_lt) + j];
-  const uint32_t u = cached_word(c, e, wc, j, SCG_STREAM_SC_LEADTIME);
-  int32_t x = 0;
-  for (int i = 0; i < c.lt_thr_len; ++i) x += (c.lt_thr[i] <= u) ? 1 : 0;
-  x += 1;
+  int32_t x;
+  if (c.lt_tab) {  // caller table (validated on the host); clamped too, so no value can
+                   // exceed the proven heap capacity or land at/before the current step
+    x = c.lt_tab[e.local * (static_cast<int64_t>(c.T) * c.n_lt) + j];
+  } else {
+    const uint32_t u = cached_word(c, e, wc, j, SCG_STREAM_SC_LEADTIME);
+    x = 0;
+    for (int i = 0; i < c.lt_thr_len; ++i) x += (c.lt_thr[i] <= u) ? 1 : 0;
+    x += 1;
+  }
   return x < 1 ? 1 : (x > c.max_lt ? c.max_lt : x);
 }
 

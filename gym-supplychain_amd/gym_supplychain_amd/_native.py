@@ -16,7 +16,7 @@ import torch  # noqa: F401  (loads the HIP runtime libscgpu.so binds to)
 
 LIB_NAME = "libscgpu.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 SCG_OK = 0
 SCG_ERR_INVALID = 1
@@ -96,7 +96,7 @@ class BgState(ctypes.Structure):
     ]
 
 
-SC_MAX_PRODUCTS = 8
+SC_MAX_PRODUCTS = 16
 SC_MAX_DESTS = 32
 SC_MAX_INIT = 16
 SC_MAX_NODES = 256

@@ -14,6 +14,7 @@ Differences from the reference, all documented in DESIGN.md:
 """
 import ctypes
 import numbers
+import os
 
 import numpy as np
 import torch
@@ -32,6 +33,15 @@ STD_INV_COST = 1
 STD_BACKLOG_COST = 2
 
 _I32 = (-(2 ** 31), 2 ** 31 - 1)
+# sampled actions of the vec envs' Box stay int32-exact over an episode (|a| <= 2^15)
+ACTION_BOUND = 2 ** 15
+
+
+def _entropy_seed(seed):
+    """A Philox key: `seed`, or fresh OS entropy for None (RandomState(None) semantics)."""
+    if seed is None:
+        return int.from_bytes(os.urandom(8), "little")
+    return int(seed) & 0xFFFFFFFFFFFFFFFF
 
 
 def _int32(name, v):
@@ -240,8 +250,8 @@ class BeerGameVecEnv:
         return self._obs
 
     def seed(self, seed=None):
-        """New Philox key; the next reset() starts episode 0 again."""
-        self._st.seed = 0 if seed is None else int(seed) & 0xFFFFFFFFFFFFFFFF
+        """New Philox key (fresh entropy for None); the next reset() starts episode 0 again."""
+        self._st.seed = _entropy_seed(seed)
         self._st.episode, self._st.week = 0, -1
 
     def _actions(self, actions):
@@ -551,7 +561,8 @@ class BeerGame2VecEnv(BeerGameVecEnv):
         if cfg.delay_range:
             fields.update(stochastic_delays=1, delay_lo=cfg.delay_range[0], delay_hi=cfg.delay_range[1])
         demand = ("uniform",) + cfg.demand_range if cfg.demand_range else "fixed"
-        super().__init__(n_envs, None, demand=demand, seed=0 if seed is None else seed, device=device,
+        # seed=None: fresh entropy, as the reference's RandomState(None) (beergame2_env.py:58)
+        super().__init__(n_envs, None, demand=demand, seed=_entropy_seed(seed), device=device,
                          env_offset=env_offset, auto_reset=auto_reset, track_costs=track_costs,
                          track_history=track_history, track_returns=track_returns, config=cfg, variant_fields=fields)
         self.max_stock, self.max_order = cfg.max_stock, cfg.max_order

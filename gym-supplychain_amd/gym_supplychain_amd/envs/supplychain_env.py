@@ -300,6 +300,10 @@ class SupplyChainVecEnv:
             if (leadtime_table.device != self.device or leadtime_table.dtype != torch.int32 or
                     tuple(leadtime_table.shape) != (n_envs, T, spec.n_leadtimes)):
                 raise ValueError(f"leadtime_table must be int32 [{n_envs}, {T}, {spec.n_leadtimes}] on {self.device}")
+            lo, hi = int(leadtime_table.min()), int(leadtime_table.max())
+            if lo < 1 or hi > spec.max_leadtime:  # the range the reference's draws have (:670-672)
+                raise ValueError(f"leadtime_table values must lie in [1, max_leadtime={spec.max_leadtime}], "
+                                 f"got [{lo}, {hi}]")
             self._lt_tab = leadtime_table.contiguous()
             c.leadtime_table = self._lt_tab.data_ptr()
         self._cfg = c
@@ -527,13 +531,57 @@ class SupplyChainVecEnv:
         pass
 
 
-class SupplyChainEnv:
+class SC_NodeView:
+    """Read-only view of one chain node of a drop-in env, with the attributes the
+    reference's SC_Node exposes and its tests read (supplychain_env.py:120-176): `stock`
+    (float64 array, :228), `shipments_by_prod` (per product, the in-transit heap as a list
+    of (time, amount) tuples in heapq storage order, :175, :398-400), capacities and costs.
+    Each access reads the device state back."""
+
+    def __init__(self, env, index):
+        self._env, self._i = env, index
+        nd = env._vec.spec.nodes[index]
+        self.label = nd["name"]
+        self.num_products = env._vec.spec.P
+        self.last_level = nd["last_level"]
+        self.stock_capacities = list(nd["stock_capacity"])
+        self.stock_cost = list(nd["stock_cost"])
+        self.max_ship = list(nd["max_ship"])
+        self.processing_capacity = nd["processing_capacity"]
+        self.num_supply_actions, self.num_ship_actions = nd["n_supply"], nd["n_ship"]
+
+    @property
+    def stock(self):
+        return self._env._vec.stock[0, self._i].cpu().numpy().copy()
+
+    @property
+    def shipments_by_prod(self):
+        return self._env._vec.heaps(0)[self._i]
+
+    def num_expected_actions(self):
+        return self.num_supply_actions + self.num_ship_actions
+
+    def is_last_level(self):
+        return self.last_level
+
+    def __repr__(self):
+        return f"{self.label} ({self.shipments_by_prod}) [{np.round(self.stock, 1)}]"
+
+
+class SupplyChainEnv(spaces.Env):
     """Drop-in for gym_supplychain.envs.SupplyChainEnv (:478-813), one env on the GPU.
 
     Same constructor keywords; reset() -> float64 obs in [-1, 1]; step(action) ->
-    (obs, np.float64 reward, done, info); seed(seed). info is {} or, with build_info,
-    {'sc_episode': ledgers} (one dict per episode, updated in place each step). Demand and stochastic lead times are
-    drawn with Philox from `seed` (see module docstring).
+    (obs, np.float64 reward, done, info); seed(seed) re-creates the RandomState and seeds
+    action_space with 0 (:811-813). info is {} or, with build_info, {'sc_episode':
+    ledgers} (one dict per episode, updated in place each step).
+
+    host_rng=True (default): each reset() draws the episode's demand and lead times from
+    the env's RandomState exactly as the reference does (:564, :644-672; envs/host_rng.py)
+    and uploads them, so seeded episodes are the reference's, draw for draw.
+    host_rng=False: Philox draws on the device from `seed` (module docstring).
+    The reference's attributes `customer_demands`, `leadtimes`, `nodes` (SC_NodeView),
+    `count_leadtimes_per_timestep` and `rand_generator` are kept.
     """
 
     def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
@@ -541,28 +589,47 @@ class SupplyChainEnv:
                  demand_config_by_product=False, demand_range=(10, 20), demand_std=None, demand_sen_peaks=None,
                  avg_demand_range=None, processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2,
                  max_leadtime=2, total_time_steps=360, seed=None, build_info=False, demand_perturb_norm=False,
-                 device=None):
+                 device=None, host_rng=True):
+        dkw = dict(demand_config_by_product=demand_config_by_product, demand_range=demand_range,
+                   demand_std=demand_std, demand_sen_peaks=demand_sen_peaks, avg_demand_range=avg_demand_range,
+                   demand_perturb_norm=demand_perturb_norm)
         spec = SupplyChainSpec(nodes_info, num_products=num_products, unmet_demand_cost=unmet_demand_cost,
                                exceeded_stock_capacity_cost=exceeded_stock_capacity_cost,
                                exceeded_process_capacity_cost=exceeded_process_capacity_cost,
                                exceeded_ship_capacity_cost=exceeded_ship_capacity_cost,
-                               demand_config_by_product=demand_config_by_product, demand_range=demand_range,
-                               demand_std=demand_std, demand_sen_peaks=demand_sen_peaks,
-                               avg_demand_range=avg_demand_range, processing_ratio=processing_ratio,
+                               processing_ratio=processing_ratio,
                                stochastic_leadtimes=stochastic_leadtimes, avg_leadtime=avg_leadtime,
                                max_leadtime=max_leadtime, total_time_steps=total_time_steps, seed=seed,
-                               build_info=build_info, demand_perturb_norm=demand_perturb_norm)
+                               build_info=build_info, **dkw)
+        T, R, P = spec.total_time_steps, spec.n_retailers, spec.P
+        self._host = None
+        vec_kw = {}
+        if host_rng:
+            from .host_rng import HostEpisodeDraws
+            self._host = HostEpisodeDraws(dkw, R, P, T, spec.n_leadtimes, spec.stochastic_leadtimes,
+                                          spec.avg_leadtime, spec.max_leadtime, seed)
+            dev = torch.device(device) if device is not None else torch.device("cuda")
+            vec_kw["demand_table"] = torch.zeros((1, T + 1, R, P), dtype=torch.int32, device=dev)
+            if spec.stochastic_leadtimes:
+                vec_kw["leadtime_table"] = torch.ones((1, T, spec.n_leadtimes), dtype=torch.int32, device=dev)
         self._vec = SupplyChainVecEnv(1, spec=spec, seed=seed, device=device, auto_reset=False,
-                                      obs_dtype=torch.float64)
+                                      obs_dtype=torch.float64, **vec_kw)
         self.num_products = spec.P
         self.total_time_steps = spec.total_time_steps
         self.stochastic_leadtimes = spec.stochastic_leadtimes
         self.avg_leadtime, self.max_leadtime = spec.avg_leadtime, spec.max_leadtime
         self.demand_range = spec.demand_range
-        self.action_space = spaces.Box(-1.0, 1.0, (spec.n_actions,), np.float32)
-        self.observation_space = spaces.Box(-1.0, 1.0, (spec.n_obs,), np.float32)
+        self.demand_config_by_product = spec.demand_config_by_product
+        if spec.stochastic_leadtimes:
+            self.count_leadtimes_per_timestep = spec.n_leadtimes                       # :601-605
+        self.action_space = spaces.Box(-1.0, 1.0, (spec.n_actions,), np.float32)   # :625
+        self.observation_space = spaces.Box(-1.0, 1.0, (spec.n_obs,), np.float32)  # :626
+        self.nodes = [SC_NodeView(self, i) for i in range(len(spec.nodes))]
+        self.last_level_nodes = [nd for nd in self.nodes if nd.last_level]
         self.current_state = None
         self.current_reward = 0
+        self.customer_demands = None
+        self.leadtimes = None
         pin = torch.cuda.is_available()
         self._act_host = torch.zeros((1, spec.n_actions), dtype=torch.float32, pin_memory=pin)
         self._act_np = self._act_host.numpy()
@@ -576,11 +643,39 @@ class SupplyChainEnv:
     def time_step(self):
         return self._vec.time_step
 
+    @property
+    def rand_generator(self):
+        """The reset-time RandomState (host_rng mode), as the reference's attribute (:564)."""
+        return self._host.rng if self._host is not None else None
+
     def seed(self, seed=None):
-        self._vec.seed(seed)
+        """:811-813 — a new RandomState(seed) for the episode draws (host_rng; the Philox key
+        otherwise), and action_space.seed(0)."""
+        if self._host is not None:
+            self._host.seed(seed)
+        else:
+            self._vec.seed(seed)
+        self.action_space.seed(0)
+
+    def _upload_episode_tables(self):
+        """Draw this episode's tables on the host (reference order) and copy them to the
+        device tables the kernels read; synchronous copies from pageable memory, so the
+        host buffers may be reused at once."""
+        dem, table, lts = self._host.draw()
+        self.customer_demands = dem
+        self._vec._dem_tab.copy_(torch.from_numpy(table).unsqueeze(0))
+        if lts is not None:
+            self.leadtimes = lts
+            self._vec._lt_tab.copy_(torch.from_numpy(lts.astype(np.int32)).unsqueeze(0))
 
     def reset(self):
+        if self._host is not None:
+            self._upload_episode_tables()
         obs = self._vec.reset()
+        if self._host is None:  # Philox draws of this episode, read back for the attributes
+            dem, lts = self._vec.draw_tables()
+            self.customer_demands = dem[0].cpu().numpy().astype(np.int64)
+            self.leadtimes = None if lts is None else lts[0].cpu().numpy().astype(np.int64)
         self.current_reward = 0
         self.episode_rewards = 0
         if self.build_info:  # a new ledger dict per episode, mutated by every step (:677-678, :796)
@@ -590,7 +685,11 @@ class SupplyChainEnv:
         return self.current_state
 
     def step(self, action):
-        self._act_np[0, :] = np.asarray(action, dtype=np.float32).reshape(-1)
+        a = np.asarray(action, dtype=np.float32).reshape(-1)
+        n = self._act_np.shape[1]
+        if a.size < n:  # the reference's per-node slices run past the end (:716-717 -> act)
+            raise IndexError(f"action has {a.size} values, the chain needs {n}")
+        self._act_np[0, :] = a[:n]  # like the reference, values beyond the chain's actions are unused
         self._act_dev.copy_(self._act_host, non_blocking=True)
         obs, rew, done, _ = self._vec.step(self._act_dev)
         self._obs_host.copy_(obs, non_blocking=True)

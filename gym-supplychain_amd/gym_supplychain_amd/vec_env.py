@@ -104,6 +104,8 @@ class SB3VecEnv(_SB3VecEnv):
         if device:
             term = info["terminal_observation"]
             rets = info.get("episode_return")
+            if rets is not None and self.monitor:  # one device->host copy, not one sync per env
+                rets = rets.cpu().tolist()
         elapsed = round(time.time() - self._t0, 6)
         infos = []
         for i in range(self.num_envs):

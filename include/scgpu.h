@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SCG_ABI_VERSION 2
+#define SCG_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define SCG_API __attribute__((visibility("default")))
@@ -212,7 +212,7 @@ SCG_API int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, 
  * demand word (t*R + r)*P + p on stream 2, lead-time word (t-1)*n_lt + k on stream 3.
  * ====================================================================================== */
 
-#define SCG_SC_MAX_PRODUCTS 8
+#define SCG_SC_MAX_PRODUCTS 16
 #define SCG_SC_MAX_DESTS 32
 #define SCG_SC_MAX_INIT 16
 #define SCG_SC_MAX_NODES 256

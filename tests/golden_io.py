@@ -52,3 +52,23 @@ def load_beergame2(name):
     g = dict(np.load(os.path.join(GOLDEN, f"beergame2_{name}.npz")))
     g["kwargs"] = ast.literal_eval(str(g["kwargs"]))
     return g
+
+
+# ---- reference pins and RandomState fixtures (written by oracle/gen_golden_pins.py) ------
+def load_ref_pins():
+    """{case: dict(meta..., rewards=[T] float64, first_actions=[2, A] float32)}"""
+    import json
+    z = np.load(os.path.join(GOLDEN, "ref_pins.npz"))
+    meta = json.loads(bytes(z["meta"]).decode())
+    for name, m in meta.items():
+        m["rewards"] = z[f"{name}/rewards"]
+        m["first_actions"] = z[f"{name}/first_actions"]
+    return meta
+
+
+def load_ref_tables():
+    """{fixture name: int64 array as stored in the reference's tests/data/<name>.npy}"""
+    import json
+    z = np.load(os.path.join(GOLDEN, "ref_tables.npz"))
+    meta = json.loads(bytes(z["meta"]).decode())
+    return {k: z[k].astype(np.int64) for k in meta}, meta
