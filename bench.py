@@ -11,18 +11,24 @@ synthetic uniform integers in [0, 8], generated on device before timing (the pol
 output, resident in HBM). Envs shard across ranks by global id; the only collective is the
 async RCCL all-gather of per-env episode returns at each episode end.
 
-Rank 0 prints ONE JSON line. `value` is the wall clock of the timed step loop, in which no
-launch is stamped. `roofline` prices the step kernel: the algorithmic bytes of the timed
-region's launches (DESIGN.md §6, 260 B per env on a regular week, summed week by week) ÷
-the timed region's GPU time, from HIP events recorded on the launch stream around the
-loop — live, and an upper bound on the kernels' duration (it also holds the boundaries
-between launches), so `achieved` is conservative. Cross-check: `isolated_kernel_us`, the
-average of `--kernel-samples` further launches (whole 35-week cycles) after the timed
-region, each stamped by hipExtLaunchKernel with its own dispatch begin/end (the interval
-rocprofv3 reports) and run alone — stamping inside the loop would slow it, and a stamped
-launch queued behind another also counts the tail of its predecessor.
-`cpu_baseline` times oracle.beergame.BeerGameOracle — the per-env NumPy restatement of the
-reference step() — on the host's cores (rank 0, N = 1 only).
+Timing (rank 0 prints ONE JSON line):
+  * warm-up: max(W, 35) untimed steps — at least one whole 35-week episode, so every week
+    kind of the plan and the auto-reset have run before timing ("warmup_steps_run");
+  * the timed region is exactly K steps, bracketed by barrier + synchronize, max over
+    ranks; `value` = envs of all ranks x K / that wall time. Nothing inside is stamped
+    except the first and the last launch, whose own dispatch begin / end timestamps
+    (hipExtLaunchKernel) give the region's GPU time: `roofline.avg_kernel_us` = that / K;
+  * `episodes_timed`: the same measurement over 100 whole episodes (3,500 steps), as
+    SURVEY §8(d) asks, reported beside the K-step headline;
+  * `roofline`: algorithmic bytes of the timed launches (DESIGN.md §6, 260 B per env on a
+    regular week, summed week by week) / their GPU time, against the 8 TB/s spec and the
+    peak a STREAM copy measures in the same run (`measured_peak`, `frac_measured_peak`);
+    `traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    kernel; `isolated_kernel_us` = launches timed one at a time; `beyond_cache` = the same
+    kernel at 1,048,576 envs (272 MB per step, past the 256 MiB Infinity Cache);
+  * `cpu_baseline` (rank 0, N = 1): oracle.beergame.BeerGameOracle — the per-env NumPy
+    restatement of the reference step(), calibrated against the reference by
+    tools/cpu_calibration.py — on the host's cores.
 """
 import argparse
 import json
@@ -40,10 +46,13 @@ WEEKS = 35
 LAMBDA = 8.0
 SEED = 0x5EED0000
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
+EPISODES_TIMED = 100   # >= 100 episodes timed
+KERNEL = "bg_step_slab_kernel<4, 2>"
+BEYOND_CACHE_ENVS = 1 << 20
 
 
 def step_bytes_per_env(plan_word, week, T, L, ring_initial_slots, ledgers, history, returns, autoreset):
-    """Algorithmic HBM bytes one env moves in one bg_step_kernel launch (mirrors the kernel).
+    """Algorithmic HBM bytes one env moves in one step launch (mirrors the kernel).
 
     Regular week of the bench config (due row arrives, scheduled row stored, ledgers,
     history and returns on): 4 rows in (action, inventory, backlog, orders) + due row +
@@ -70,23 +79,54 @@ def step_bytes_per_env(plan_word, week, T, L, ring_initial_slots, ledgers, histo
     return b
 
 
-def pmc_traffic(kernel_substr="bg_step_kernel<4, 2>", n_envs=N_ENVS):
-    """HBM bytes per launch of the step kernel from the latest committed PMC summary
-    (profiles/rNN_pmc_summary.json, written by tools/pmc_summary.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench at 65,536 envs; FETCH_SIZE
-    doubled per MI355X_MICROARCH.md §HBM). None when absent or for another batch size."""
+def pmc_traffic(kernel_substr=KERNEL, n_envs=N_ENVS):
+    """HBM bytes per launch of the step kernel from the latest committed PMC summary that
+    has it (profiles/rNN*_pmc_summary.json, tools/pmc_summary.py, separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench at 65,536 envs; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md §HBM). None when absent or for another batch size."""
     import glob
     if n_envs != N_ENVS:
         return None, None
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        traffic = json.load(f).get("traffic", {})
-    for name, t in traffic.items():
-        if kernel_substr in name and t.get("hbm_bytes_per_launch"):
-            return t["hbm_bytes_per_launch"], os.path.relpath(files[-1], REPO)
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
+        with open(path) as f:
+            traffic = json.load(f).get("traffic", {})
+        for name, t in traffic.items():
+            if kernel_substr in name and t.get("hbm_bytes_per_launch"):
+                return t["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
     return None, None
+
+
+# ---- CPU baseline ------------------------------------------------------------------------
+def cpu_worker_inputs(idx, n_episodes):
+    """Per-episode inputs of CPU worker `idx`, drawn before timing: Poisson(8) demand lists
+    (the device's Philox draws of env `idx`) and uniform [0, 8] actions [E, 35, L]."""
+    import numpy as np
+
+    from oracle.philox import STREAM_DEMAND, draw_words
+    from oracle.poisson import poisson_invert, poisson_thresholds
+    thr = poisson_thresholds(LAMBDA)
+    demands = [poisson_invert(draw_words(SEED, [idx], ep, WEEKS, STREAM_DEMAND), thr)[0].tolist()
+               for ep in range(n_episodes)]
+    acts = np.random.RandomState(idx).randint(0, 9, size=(n_episodes, WEEKS, LEVELS))
+    return demands, acts
+
+
+def _cpu_worker(arg):
+    idx, budget_s = arg
+    sys.path.insert(0, REPO)
+    from oracle.beergame import BeerGameOracle
+    demands, acts = cpu_worker_inputs(idx, 64)
+    steps, ep = 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:  # construct + reset + 35 steps per episode
+        k = ep % len(demands)
+        env = BeerGameOracle({"customer_demand": demands[k]})
+        env.reset()
+        for w in range(WEEKS):
+            env.step(acts[k, w])
+        steps += WEEKS
+        ep += 1
+    return steps, time.perf_counter() - t0
 
 
 def cpu_baseline(budget_s=1.5, max_procs=16):
@@ -103,32 +143,130 @@ def cpu_baseline(budget_s=1.5, max_procs=16):
     steps = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x {budget_s:.1f} s of beergame-v0 episodes (35 weeks, Poisson(8) "
-                      f"demand, uniform [0,8] actions), one env per process, oracle.beergame.BeerGameOracle; "
-                      f"{steps} env-steps total"}
+            "sample": f"{procs} processes x {budget_s:.1f} s of beergame-v0 episodes (construct + reset + 35 steps; "
+                      f"Poisson(8) demand, uniform [0,8] actions drawn before timing), one env per process, "
+                      f"oracle.beergame.BeerGameOracle (the reference step() statement for statement; "
+                      f"profiles/r02_cpu_calibration.json); {steps} env-steps total"}
 
 
-def _cpu_worker(arg):
-    idx, budget_s = arg
-    import numpy as np
-    sys.path.insert(0, REPO)
-    from oracle.beergame import BeerGameOracle
-    from oracle.philox import STREAM_DEMAND, draw_words
-    from oracle.poisson import poisson_invert, poisson_thresholds
-    thr = poisson_thresholds(LAMBDA)
-    rng = np.random.RandomState(idx)
-    steps, ep = 0, 0
+# ---- the step loop (GPU VecEnv, or a CPU stand-in in tests/test_bench_distributed.py) -----
+class StepLoop:
+    """Steps `env` with the resident action row of each week; at episode ends hands the
+    finished returns to `gather` (the async all-gather)."""
+
+    def __init__(self, env, week_actions, gather=None):
+        self.env, self.week_actions, self.gather = env, week_actions, gather
+        self.episodes = 0
+
+    def run(self, k, first=None, last=None, each=None, sync_each=None):
+        env, acts = self.env, self.week_actions
+        for i in range(k):
+            stamp = each[i] if each is not None else ((first, None) if i == 0 and first else None)
+            if i == k - 1 and last is not None:
+                stamp = (stamp[0] if stamp else None, last)
+            _, _, _, info = env.step(acts[env.week], stamp) if stamp else env.step(acts[env.week])
+            if info:
+                self.episodes += 1
+                if self.gather is not None:
+                    self.gather.on_episode_end(info["episode_return"])
+            if sync_each is not None:
+                sync_each()
+
+
+def region(loop, k, world, barrier, sync, stamps=None):
+    """Time exactly k steps: barrier + sync on both sides. Returns (wall s, GPU ms between
+    the first launch's start and the last one's end, or None without stamps)."""
+    if world > 1:
+        barrier()
+    sync()
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        demand = poisson_invert(draw_words(SEED, [idx], ep, WEEKS, STREAM_DEMAND), thr)[0]
-        acts = rng.randint(0, 9, size=(WEEKS, LEVELS))
-        env = BeerGameOracle({"customer_demand": demand.tolist()})
-        env.reset()
-        for w in range(WEEKS):
-            env.step(acts[w])
-        steps += WEEKS
-        ep += 1
-    return steps, time.perf_counter() - t0
+    loop.run(k, first=stamps[0] if stamps else None, last=stamps[1] if stamps else None)
+    sync()
+    if world > 1:
+        barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = stamps[2](stamps[0], stamps[1]) if stamps else None
+    return elapsed, gpu_ms
+
+
+def max_over_ranks(values, world, device):
+    """Elementwise max of a list of floats over ranks (all_reduce MAX; None stays None)."""
+    if world == 1:
+        return values
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([-1.0 if v is None else float(v) for v in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [None if v is None else float(x) for v, x in zip(values, t.tolist())]
+
+
+def stream_copy_peak(device, nbytes=1 << 30, iters=20):
+    """Achievable HBM bandwidth: scg_stream_copy of nbytes (past every cache), GB/s of
+    read + write traffic averaged over `iters` back-to-back copies."""
+    import ctypes
+
+    import torch
+
+    from gym_supplychain_amd import _native as nat
+    src = torch.empty(nbytes // 4, dtype=torch.int32, device=device).fill_(7)
+    dst = torch.empty_like(src)
+    stream = torch.cuda.current_stream(device)
+    blocks = 256 * 32      # 32 workgroups (128 waves) per CU over the copy, 4 loads in flight per lane
+
+    def copy():
+        nat.check(nat.lib.scg_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, blocks,
+                                          ctypes.c_void_p(stream.cuda_stream)))
+    copy()
+    torch.cuda.synchronize(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        copy()
+    e1.record(stream)
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / iters
+    assert bool((dst[:: (1 << 20)] == 7).all())
+    del src, dst
+    return 2 * nbytes / (ms / 1e3) / 1e9
+
+
+def beyond_cache_point(device, n_envs=BEYOND_CACHE_ENVS, episodes=2):
+    """The bench kernel at n_envs (one step = 272 MB at 2^20 envs, past the 256 MiB
+    Infinity Cache): GPU timeline of `episodes` whole episodes after one warm-up episode."""
+    import ctypes
+
+    import torch
+
+    from gym_supplychain_amd import BeerGameVecEnv
+    from gym_supplychain_amd import _native as nat
+    env = BeerGameVecEnv(n_envs, {}, demand="poisson", poisson_lambda=LAMBDA, seed=SEED, device=device,
+                         auto_reset=True, track_costs=True, track_history=True, track_returns=True)
+    stream = torch.cuda.current_stream(device)
+    acts = torch.empty((WEEKS, n_envs, LEVELS), dtype=torch.int32, device=device)
+    nat.check(nat.lib.scg_uniform_ints(SEED, 0, n_envs, WEEKS, LEVELS, 0, 0, 8, acts.data_ptr(),
+                                       ctypes.c_void_p(stream.cuda_stream)))
+    week = list(acts.unbind(0))
+    env.reset()
+    for _ in range(WEEKS):
+        env.step(week[env.week])
+    plan = list(env._plan)
+    k = episodes * WEEKS
+    nbytes = sum(n_envs * step_bytes_per_env(plan[w % WEEKS + 1], w % WEEKS + 1, WEEKS, LEVELS, 2, True, True, True,
+                                             True) for w in range(k))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    e0.record(stream)
+    for _ in range(k):
+        env.step(week[env.week])
+    e1.record(stream)
+    torch.cuda.synchronize(device)
+    env.check_errors()
+    ms = e0.elapsed_time(e1)
+    del env, acts, week
+    torch.cuda.empty_cache()
+    return {"n_envs": n_envs, "steps": k, "avg_kernel_us": ms * 1e3 / k, "bytes_per_launch": nbytes / k,
+            "achieved": nbytes / (ms / 1e3) / 1e9, "frac": nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+            "env_steps_per_s_gpu": n_envs * k / (ms / 1e3)}
 
 
 def main():
@@ -138,6 +276,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=350)
     ap.add_argument("--envs", type=int, default=N_ENVS, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the STREAM peak and beyond-cache point")
     ap.add_argument("--cpu-budget", type=float, default=1.5)
     ap.add_argument("--kernel-samples", type=int, default=350,
                     help="launches timed one at a time with kernel-stamped events after the timed region")
@@ -171,72 +310,75 @@ def main():
                                        ctypes.c_void_p(stream.cuda_stream)))
     gather = EpisodeReturnGather(N, device)
     env.reset()
-
-    week_actions = list(actions.unbind(0))  # the policy output of each week, resident in HBM
-
-    def run(k, events=None, isolated=False):
-        for i in range(k):
-            _, _, done, info = env.step(week_actions[env.week], None if events is None else events[i])
-            if info:
-                gather.on_episode_end(info["episode_return"])
-            if isolated:
-                torch.cuda.synchronize(device)
+    loop = StepLoop(env, list(actions.unbind(0)), gather)  # the policy output of each week, resident in HBM
+    plan = list(env._plan)
 
     def week_bytes(w):
         return N * step_bytes_per_env(plan[w], w, WEEKS, LEVELS, 2, True, True, True, True)
 
-    run(args.warmup)
-    plan = list(env._plan)
-    w_timed = env.week  # the timed region's launches run weeks w_timed+1, w_timed+2, ... (mod 35)
-    timed_bytes = sum(week_bytes((w_timed + i) % WEEKS + 1) for i in range(args.steps))
-    # timed region: plain launches, nothing stamped; GPU-timeline events on the launch stream
-    # (torch's current stream, which VecEnv.step launches on) bracket it
-    t_ev0, t_ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    t_ev0.record(stream)
-    run(args.steps)
-    t_ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def bytes_of(k):  # launches run weeks env.week+1, +2, ... (mod 35)
+        w0 = env.week
+        return sum(week_bytes((w0 + i) % WEEKS + 1) for i in range(k))
+
+    def sync():
+        torch.cuda.synchronize(device)
+
+    barrier = dist.barrier if world > 1 else None
+    ev = [nat.hip_event() for _ in range(4)]
+
+    warmup_run = max(args.warmup, WEEKS)
+    loop.run(warmup_run)
+    # headline: exactly K steps
+    timed_bytes = bytes_of(args.steps)
+    elapsed, gpu_ms = region(loop, args.steps, world, barrier, sync, (ev[0], ev[1], nat.hip_event_elapsed_ms))
     gather.result()
-    torch.cuda.synchronize()
-    timeline_ms = t_ev0.elapsed_time(t_ev1)
-    # kernel duration: a further `--kernel-samples` launches (a multiple of the 35-week cycle,
-    # so every week kind is weighted as in the timed region), each stamped with its own
-    # dispatch begin/end by hipExtLaunchKernel (the interval rocprofv3 reports) and run
-    # alone: a stamped launch queued behind another would also count its predecessor's tail
+    # 100 whole episodes, from an episode boundary
+    loop.run((WEEKS - env.week) % WEEKS)
+    k_ep = EPISODES_TIMED * WEEKS
+    ep_bytes = bytes_of(k_ep)
+    ep_elapsed, ep_gpu_ms = region(loop, k_ep, world, barrier, sync, (ev[2], ev[3], nat.hip_event_elapsed_ms))
+    gather.result()
+    # isolated launches: whole 35-week cycles, each stamped and run alone
     k_samples = max(WEEKS, args.kernel_samples // WEEKS * WEEKS)
-    w0 = env.week
-    sampled_bytes = sum(week_bytes((w0 + i) % WEEKS + 1) for i in range(k_samples))
-    events = [(nat.hip_event(), nat.hip_event()) for _ in range(k_samples)]
-    run(k_samples, events, isolated=True)
-    kern_ms = sum(nat.hip_event_elapsed_ms(s, e) for s, e in events)
-    for s, e in events:
-        nat.hip_event_destroy(s)
+    sampled_bytes = bytes_of(k_samples)
+    iso = [(nat.hip_event(), nat.hip_event()) for _ in range(k_samples)]
+    loop.run(k_samples, each=iso, sync_each=sync)
+    iso_ms = sum(nat.hip_event_elapsed_ms(s, e) for s, e in iso)
+    for e in ev + [x for pair in iso for x in pair]:
         nat.hip_event_destroy(e)
-    n_sampled = k_samples
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms, timeline_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, timeline_ms = float(t[0]), float(t[1]), float(t[2])
+    env.check_errors()
+    elapsed, gpu_ms, ep_elapsed, ep_gpu_ms, iso_ms = max_over_ranks([elapsed, gpu_ms, ep_elapsed, ep_gpu_ms, iso_ms],
+                                                                     world, device)
+    extras = {}
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras["measured_peak"] = stream_copy_peak(device)
+        extras["beyond_cache"] = beyond_cache_point(device)
 
     if rank == 0:
-        value = N * world * args.steps / elapsed
-        avg_kernel_s = timeline_ms / 1e3 / args.steps
-        achieved = timed_bytes / (timeline_ms / 1e3) / 1e9
+        achieved = timed_bytes / (gpu_ms / 1e3) / 1e9
         traffic, traffic_src = pmc_traffic(n_envs=N)
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": f"scg::{KERNEL} (L = 4, Poisson demand, state slab)",
+                "avg_kernel_us": gpu_ms * 1e3 / args.steps,
+                "avg_kernel_source": "first launch's dispatch begin to last launch's end (hipExtLaunchKernel stamps) "
+                                     "over the timed region",
+                "bytes_per_launch": timed_bytes / args.steps, "launches_timed": args.steps,
+                "isolated_kernel_us": iso_ms * 1e3 / k_samples, "isolated_launches": k_samples,
+                "isolated_frac": sampled_bytes / (iso_ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+        if "measured_peak" in extras:
+            roof["measured_peak"] = extras["measured_peak"]
+            roof["frac_measured_peak"] = achieved / extras["measured_peak"]
+            roof["measured_peak_source"] = "scg_stream_copy of 1 GiB (read + write), 20 launches, same run"
+            roof["beyond_cache"] = extras["beyond_cache"]
         line = {
             "metric": "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X",
-            "value": value,
+            "value": N * world * args.steps / elapsed,
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_steps_run": warmup_run,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
@@ -247,13 +389,10 @@ def main():
                        "n_envs_per_gpu": N, "levels": LEVELS, "weeks": WEEKS, "auto_reset": True,
                        "ledgers": True, "orders_history": True, "episode_return_allgather": world > 1,
                        "parallelism": f"env-shard x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "scg::bg_step_kernel<4, 2> (L = 4, Poisson demand)", "avg_kernel_us": avg_kernel_s * 1e6,
-                         "avg_kernel_source": "HIP events on the launch stream around the timed region",
-                         "bytes_per_launch": timed_bytes / args.steps, "launches_timed": args.steps,
-                         "isolated_kernel_us": kern_ms * 1e3 / n_sampled, "isolated_launches": n_sampled,
-                         "isolated_frac": sampled_bytes / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "episodes_timed": {"episodes": EPISODES_TIMED, "steps": k_ep, "value": N * world * k_ep / ep_elapsed,
+                               "ms_per_step": ep_elapsed * 1e3 / k_ep, "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
+                               "frac": ep_bytes / (ep_gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)

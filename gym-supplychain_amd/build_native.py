@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "gym_supplychain_amd", "libscgpu.so")
-SOURCES = ["scg_common.hip", "scg_beergame.hip", "scg_supplychain.hip"]
+SOURCES = ["scg_common.hip", "scg_beergame.hip", "scg_bg_levels_1.hip", "scg_bg_levels_2.hip", "scg_bg_levels_3.hip",
+           "scg_bg_levels_4.hip", "scg_supplychain.hip"]
 ARCH = "gfx950"
 
 
@@ -50,11 +51,38 @@ def build(debug=False, verbose=True):
 
 
 # hipcc flags of libscgpu.so (tools/exp_build.py builds its variants with the same ones)
-HIP_FLAGS = ["-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-ffp-contract=off",
+HIP_FLAGS = ["-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
              # leading scalar kernel arguments preloaded into SGPRs at wave launch (gfx950);
              # kernels whose first argument is a struct are unaffected
-             "-mllvm", "-amdgpu-kernarg-preload-count=7",
+             "-mllvm", "-amdgpu-kernarg-preload-count=9",
              "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function"]
+
+
+def compile_library(out, srcs, include_dirs, extra=(), opt="-O3", verbose=True):
+    """Each source to an object concurrently (the template instantiations dominate), then one
+    shared-library link; the TUs share no device symbols, so no relocatable device code."""
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    inc = [x for d in include_dirs for x in ("-I", d)]
+    objs = [os.path.join(objdir, os.path.splitext(os.path.basename(s))[0] + ".o") for s in srcs]
+
+    def cc(src_obj):
+        src, obj = src_obj
+        cmd = [hipcc(), f"--offload-arch={ARCH}"] + HIP_FLAGS + inc + [opt, *extra, "-c", src, "-o", obj]
+        if verbose:
+            print("[build_native]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    with ThreadPoolExecutor(max_workers=min(len(srcs), os.cpu_count() or 1)) as pool:
+        list(pool.map(cc, zip(srcs, objs)))
+    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+    if verbose:
+        print("[build_native]", " ".join(link), flush=True)
+    subprocess.run(link, check=True)
+    os.replace(out + ".tmp", out)
+    shutil.rmtree(objdir, ignore_errors=True)
+    return out
 
 
 def build_library(debug=False, verbose=True):
@@ -65,13 +93,8 @@ def build_library(debug=False, verbose=True):
         if verbose:
             print(f"[build_native] {OUT} up to date")
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}"] + HIP_FLAGS + [
-        "-I", os.path.join(REPO, "include"), "-I", CSRC, "-O1" if debug else "-O3", "-o", OUT + ".tmp"] + srcs
-    if verbose:
-        print("[build_native]", " ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    return compile_library(OUT, srcs, [os.path.join(REPO, "include"), CSRC], opt="-O1" if debug else "-O3",
+                           verbose=verbose)
 
 
 if __name__ == "__main__":

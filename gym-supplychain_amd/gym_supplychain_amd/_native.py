@@ -93,7 +93,15 @@ class BgState(ctypes.Structure):
         ("episode_return", ctypes.c_void_p),
         ("final_return", ctypes.c_void_p),
         ("penalty_costs", ctypes.c_void_p),
+        ("error_flags", ctypes.c_void_p),
+        ("error_host", ctypes.c_void_p),
+        ("slab", ctypes.c_void_p),
     ]
+
+
+# scg_bg_slab_field: word offsets of a BeerGame state slab (scg_bg_slab_layout)
+(SLAB_ERROR, SLAB_INVENTORY, SLAB_BACKLOG, SLAB_ORDERS, SLAB_INV_COSTS, SLAB_BACKLOG_COSTS, SLAB_TERMINAL_OBS,
+ SLAB_RING, SLAB_EPISODE_RETURN, SLAB_FINAL_RETURN, SLAB_HISTORY, SLAB_TOTAL, SLAB_FIELDS) = range(13)
 
 
 SC_MAX_PRODUCTS = 16
@@ -163,6 +171,7 @@ SIGNATURES = {
     "scg_bg_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
     "scg_poisson_table": (ctypes.c_int, [ctypes.c_double, _u32p, ctypes.c_int32]),
     "scg_bg_prepare": (ctypes.c_int, [ctypes.POINTER(BgConfig)]),
+    "scg_bg_slab_layout": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.c_int64, ctypes.c_int32, _i64p]),
     "scg_bg_reset": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
                                     ctypes.c_void_p]),
     "scg_bg_step": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
@@ -185,6 +194,8 @@ SIGNATURES = {
                                    ctypes.c_void_p]),
     "scg_sc_draw_tables": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.c_uint32,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "scg_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.c_void_p]),
     "scg_uniform_ints": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                         ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_void_p, ctypes.c_void_p]),
@@ -279,6 +290,41 @@ def hip_runtime():
         _hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
         _hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
     return _hip
+
+
+class MappedWord:
+    """One int32 of pinned host memory the GPU can write (hipHostMalloc, mapped): `dev` is
+    its device address for kernels, `value` reads it on the host without synchronising."""
+
+    def __init__(self):
+        hip = hip_runtime()
+        hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        hip.hipHostFree.argtypes = [ctypes.c_void_p]
+        hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+        host = ctypes.c_void_p()
+        if hip.hipHostMalloc(ctypes.byref(host), 64, 0x2) != 0:  # hipHostMallocMapped
+            raise RuntimeError("hipHostMalloc failed")
+        dev = ctypes.c_void_p()
+        if hip.hipHostGetDevicePointer(ctypes.byref(dev), host, 0) != 0:
+            hip.hipHostFree(host)
+            raise RuntimeError("hipHostGetDevicePointer failed")
+        self._hip, self.host, self.dev = hip, host.value, dev.value
+        self._word = ctypes.c_int32.from_address(self.host)
+        self._word.value = 0
+
+    @property
+    def value(self):
+        return self._word.value
+
+    @value.setter
+    def value(self, v):
+        self._word.value = int(v)
+
+    def __del__(self):
+        try:
+            self._hip.hipHostFree(ctypes.c_void_p(self.host))
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass
 
 
 def hip_event():

@@ -15,6 +15,7 @@ Differences from the reference, all documented in DESIGN.md:
 import ctypes
 import numbers
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -117,11 +118,17 @@ class BeerGameVecEnv:
             a device tensor int32 [T, N] — caller-supplied per-env demand.
     env_offset: global id of env 0 — shards on several GPUs draw the same per-env
             demand as one big batch would (multi-GPU invariant).
+    state_slab: hold the state in one slab (scg_bg_slab_layout) so step() runs the slab
+            kernel (default; needs N * L % 4 == 0, else separate buffers and the general
+            kernel). Both give identical results.
+    Values the reference keeps in int64 are int32 here; a step whose int64 result leaves
+    int32 sets a sticky device flag, raised as OverflowError by check_errors() and, one
+    episode late (so the step loop never stalls), by the terminal step.
     """
 
     def __init__(self, n_envs, env_init_info=None, demand="fixed", poisson_lambda=8.0, seed=0, device=None,
                  env_offset=0, auto_reset=True, track_costs=True, track_history=False, track_returns=True,
-                 horizon=None, config=None, variant_fields=None):
+                 horizon=None, config=None, variant_fields=None, state_slab=True):
         n_envs = int(n_envs)
         if n_envs < 1:
             raise ValueError("n_envs must be >= 1")
@@ -193,25 +200,54 @@ class BeerGameVecEnv:
         self._cfg = c
         self.ring_slots = R = c.ring_slots
 
-        # device state, env-major [N][L] int32 (DESIGN.md "Layout in HBM")
-        self._inv = torch.zeros((n_envs, L), **i32)
-        self._bk = torch.zeros((n_envs, L), **i32)
-        self._op = torch.zeros((n_envs, L), **i32)
-        self._ring = torch.zeros((R, n_envs, L), **i32)
-        self._inv_costs = torch.zeros((n_envs, L), **i32) if track_costs else None
-        self._bk_costs = torch.zeros((n_envs, L), **i32) if track_costs else None
-        self._hist = torch.zeros((T + 1, n_envs, L), **i32) if track_history else None
-        self._ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
-        self._final_ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
+        # device state, env-major [N][L] int32 (DESIGN.md "Layout in HBM"): one slab holding
+        # every row at the offsets scg_bg_slab_layout gives (the slab step kernel addresses
+        # them all from one base), or separate tensors when N * L is not a multiple of 4
         v2 = c.variant == 2
+        off = (ctypes.c_int64 * nat.SLAB_FIELDS)()
+        self._slab = None
+        if state_slab and nat.lib.scg_bg_slab_layout(ctypes.byref(c), n_envs, int(bool(track_history)), off) == 0:
+            self._slab = torch.zeros(off[nat.SLAB_TOTAL], **i32)
+
+            def rows(field, k=1):
+                return self._slab[off[field]: off[field] + k * n_envs * L].view(*((k,) if k > 1 else ()), n_envs, L)
+
+            def i64(field):
+                return self._slab[off[field]: off[field] + 2 * n_envs].view(torch.int64)
+
+            self._err = self._slab[off[nat.SLAB_ERROR]: off[nat.SLAB_ERROR] + 1]
+            self._inv, self._bk, self._op = rows(nat.SLAB_INVENTORY), rows(nat.SLAB_BACKLOG), rows(nat.SLAB_ORDERS)
+            self._ring = rows(nat.SLAB_RING, R) if R > 1 else rows(nat.SLAB_RING).unsqueeze(0)
+            self._inv_costs = rows(nat.SLAB_INV_COSTS) if track_costs else None
+            self._bk_costs = rows(nat.SLAB_BACKLOG_COSTS) if track_costs else None
+            self._hist = rows(nat.SLAB_HISTORY, T + 1) if track_history else None
+            self._ret = i64(nat.SLAB_EPISODE_RETURN) if track_returns else None
+            self._final_ret = i64(nat.SLAB_FINAL_RETURN) if track_returns else None
+            self._term_obs = rows(nat.SLAB_TERMINAL_OBS)
+        else:
+            self._err = torch.zeros(1, **i32)
+            self._inv = torch.zeros((n_envs, L), **i32)
+            self._bk = torch.zeros((n_envs, L), **i32)
+            self._op = torch.zeros((n_envs, L), **i32)
+            self._ring = torch.zeros((R, n_envs, L), **i32)
+            self._inv_costs = torch.zeros((n_envs, L), **i32) if track_costs else None
+            self._bk_costs = torch.zeros((n_envs, L), **i32) if track_costs else None
+            self._hist = torch.zeros((T + 1, n_envs, L), **i32) if track_history else None
+            self._ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
+            self._final_ret = torch.zeros(n_envs, dtype=torch.int64, device=dev) if track_returns else None
+            self._term_obs = torch.zeros((n_envs, L), **i32)
         self._pen_costs = torch.zeros((n_envs, L), **i32) if (track_costs and v2) else None
-        # outputs: obs and reward share one allocation so N=1 callers copy back once
+        # outputs: obs and reward share one allocation so N=1 callers copy back once (and the
+        # slab kernel writes both from one preloaded base)
         self._out = torch.zeros(n_envs * L + n_envs, **i32)
         self._obs = self._out[: n_envs * L].view(n_envs, L)
         self._rew = self._out[n_envs * L:]
-        self._term_obs = torch.zeros((n_envs, L), **i32)
         self._done_false = torch.zeros(n_envs, dtype=torch.bool, device=dev)
         self._done_true = torch.ones(n_envs, dtype=torch.bool, device=dev)
+        # int32 overflow word: each terminal-week launch copies it to host-mapped memory, and
+        # the host reads that copy at terminal steps (check_errors() reads the device word),
+        # so the check never stalls the step pipeline
+        self._err_word = nat.MappedWord()
 
         s = nat.BgState()
         s.n_envs, s.env_offset, s.seed = n_envs, int(env_offset), int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -224,6 +260,9 @@ class BeerGameVecEnv:
         s.episode_return = self._ret.data_ptr() if track_returns else None
         s.final_return = self._final_ret.data_ptr() if track_returns else None
         s.penalty_costs = self._pen_costs.data_ptr() if self._pen_costs is not None else None
+        s.error_flags = self._err.data_ptr()
+        s.error_host = self._err_word.dev
+        s.slab = self._slab.data_ptr() if self._slab is not None else None
         self._st = s
         self._cfg_ref = ctypes.byref(self._cfg)
         self._st_ref = ctypes.byref(self._st)
@@ -235,11 +274,15 @@ class BeerGameVecEnv:
         self._term_ptr = self._term_obs.data_ptr()
         self._cfg_addr, self._st_addr = ctypes.addressof(self._cfg), ctypes.addressof(self._st)
         self._fast_step, self._fast_step_timed = nat.fast.bg_step, nat.fast.bg_step_timed
+        self._ready = {}  # id(actions) -> (weakref, data_ptr) of validated action tensors
         # gym surface (an extension: the reference leaves both spaces unset, :62-64)
         self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
-        self.single_action_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
+        # actions: the reference's are unbounded int64 (:121); sampled ones stay within
+        # +-ACTION_BOUND so an episode's int32 state cannot overflow (the error flag catches
+        # any caller action that does)
+        self.single_action_space = spaces.Box(-ACTION_BOUND, ACTION_BOUND - 1, (L,), np.int32)
         self.observation_space = spaces.Box(_I32[0], _I32[1], (n_envs, L), np.int32)
-        self.action_space = spaces.Box(_I32[0], _I32[1], (n_envs, L), np.int32)
+        self.action_space = spaces.Box(-ACTION_BOUND, ACTION_BOUND - 1, (n_envs, L), np.int32)
 
     # -------------------------------------------------------------------------------
     def _stream(self):
@@ -273,23 +316,50 @@ class BeerGameVecEnv:
                 and a.get_device() == self._dev_index and a.shape == self._act_shape and a.is_contiguous())
 
     def step(self, actions, _events=None):
-        if not self._is_ready(actions):
-            actions = self._actions(actions)
+        # a tensor validated once is recognised by identity and data pointer (the policy's
+        # per-week action buffers are reused), skipping the per-call checks
+        ok = self._ready.get(id(actions))
+        if ok is not None and ok[0]() is actions and ok[1] == actions.data_ptr():
+            ptr = ok[1]
+        else:
+            if self._is_ready(actions):
+                if len(self._ready) >= 64:
+                    self._ready.clear()
+                self._ready[id(actions)] = (weakref.ref(actions), actions.data_ptr())
+            else:
+                actions = self._actions(actions)
+            ptr = actions.data_ptr()
         if _events is None:
-            r = self._fast_step(self._cfg_addr, self._st_addr, actions.data_ptr(), self._obs_ptr, self._rew_ptr,
+            r = self._fast_step(self._cfg_addr, self._st_addr, ptr, self._obs_ptr, self._rew_ptr,
                                 self._term_ptr, self._flags, nat.raw_stream(self._dev_index))
         else:  # (start, stop) hipEvent_t handles stamped with the kernel's own dispatch times
-            r = self._fast_step_timed(self._cfg_addr, self._st_addr, actions.data_ptr(), self._obs_ptr,
+            r = self._fast_step_timed(self._cfg_addr, self._st_addr, ptr, self._obs_ptr,
                                       self._rew_ptr, self._term_ptr, self._flags, _events[0], _events[1],
                                       nat.raw_stream(self._dev_index))
         if r > 1:
             nat.check(r >> 1)
         if r & 1:
+            self._poll_errors()
             info = {"terminal_observation": self._term_obs}
             if self._final_ret is not None:
                 info["episode_return"] = self._final_ret
             return self._obs, self._rew, self._done_true, info
         return self._obs, self._rew, self._done_false, {}
+
+    def _poll_errors(self):
+        """At a terminal step: raise if the overflow word an earlier terminal launch exported
+        to host-mapped memory is set (no synchronisation: a launch still in flight reports
+        at a later terminal step, or check_errors() reports at once)."""
+        if self._err_word.value:
+            raise OverflowError("a BeerGame value left int32 range (the reference's int64 state would differ); "
+                                "results since then are invalid")
+
+    def check_errors(self):
+        """Raise OverflowError if any step so far produced a value outside int32 (the
+        reference computes in int64; beergame_env.py:33,35,130-132). Synchronises."""
+        if int(self._err.item()):
+            raise OverflowError("a BeerGame value left int32 range (the reference's int64 state would differ); "
+                                "results since then are invalid")
 
     def rollout(self, actions, obs_out=None, rewards_out=None):
         """K weeks in as few launches as possible (state kept in registers).
@@ -379,7 +449,7 @@ class BeerGameVecEnv:
         pass
 
 
-class BeerGameEnv:
+class BeerGameEnv(spaces.Env):
     """Drop-in for gym_supplychain.envs.BeerGameEnv (beergame_env.py:6-181), one env.
 
     Same constructor, reset()/step()/render()/close() and NumPy return types: reset()
@@ -409,6 +479,8 @@ class BeerGameEnv:
         self._act_dev = torch.zeros((1, self.levels), dtype=torch.int32, device=self._vec.device)
         self._out_host = torch.zeros(self._vec._out.shape, dtype=torch.int32, pin_memory=pin)
         self._out_np = self._out_host.numpy()
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
+        self._err_np = self._err_host.numpy()
         self.week = None
 
     def reset(self):
@@ -427,7 +499,10 @@ class BeerGameEnv:
         self._act_dev.copy_(self._act_host, non_blocking=True)
         obs, _, done, _ = self._vec.step(self._act_dev)
         self._out_host.copy_(self._vec._out, non_blocking=True)
+        self._err_host.copy_(self._vec._err, non_blocking=True)
         torch.cuda.current_stream(self._vec.device).synchronize()
+        if int(self._err_np[0]):  # the reference's int64 values no longer fit the int32 state
+            raise OverflowError("a BeerGame value left int32 range; the GPU state no longer matches the reference")
         L = self.levels
         self.week = self._vec.week
         self.current_state = self._out_np[:L].astype(np.int64)
@@ -574,7 +649,7 @@ class BeerGame2VecEnv(BeerGameVecEnv):
         raise NotImplementedError("rollout is not implemented for BeerGameEnv2")
 
 
-class BeerGameEnv2:
+class BeerGameEnv2(spaces.Env):
     """Drop-in for gym_supplychain.envs.BeerGameEnv2 (beergame2_env.py:5-211), one env.
 
     reset() -> int64 observation; step(action) -> (int64 obs, Python int reward, bool, {});
@@ -591,8 +666,8 @@ class BeerGameEnv2:
                                     initial_shipment, initial_orders, seed=seed, device=device, auto_reset=False,
                                     track_costs=True, track_history=True, track_returns=False)
         self.levels, self.max_stock, self.max_weeks = levels, max_stock, weeks
-        self.action_space = spaces.Box(0, max_order - 1, (levels,), np.int64)
-        self.observation_space = spaces.Box(0, 2 * max_stock - 1, (levels,), np.int64)
+        self.action_space = spaces.MultiDiscrete(levels * [max_order])               # :27
+        self.observation_space = spaces.MultiDiscrete(levels * [2 * max_stock])      # :28
         self.current_state = None
         self.week = None
         pin = torch.cuda.is_available()

@@ -123,7 +123,44 @@ typedef struct scg_bg_state {
   int64_t* episode_return;  /* [N] running sum of rewards (optional)                   */
   int64_t* final_return;    /* [N] episode_return at the terminal week (optional)      */
   int32_t* penalty_costs;   /* [N][L]  v2 self.penalty_costs :184 (optional)           */
+  /* Sticky DEVICE int32 error word (optional): bit 0 is set by any kernel whose int64
+   * result (state, pipeline row, ledger, observation or reward; the reference computes in
+   * int64, beergame_env.py:33,35,130-132) does not fit the int32 it is stored in. The
+   * stored values are then invalid; the flag stays set until the caller clears it. */
+  int32_t* error_flags;
+  /* Optional HOST-mapped int32 (pinned, device-accessible): every terminal-week launch copies
+   * error_flags there as the launch starts, so a host can poll earlier episodes' overflow
+   * without synchronising (read it after a later episode's terminal step has completed). */
+  int32_t* error_host;
+  /* Optional state slab (scg_bg_slab_layout): when non-NULL, every buffer above must be
+   * the slab view the layout names, and scg_bg_step launches the slab step kernel, which
+   * addresses every row from this one base. */
+  int32_t* slab;
 } scg_bg_state;
+
+/* Slab fields, in order: word offsets filled by scg_bg_slab_layout. */
+enum scg_bg_slab_field {
+  SCG_SLAB_ERROR = 0,     /* int32 error word (16-byte header)              */
+  SCG_SLAB_INVENTORY,     /* [N][L]                                          */
+  SCG_SLAB_BACKLOG,       /* [N][L]                                          */
+  SCG_SLAB_ORDERS,        /* [N][L]                                          */
+  SCG_SLAB_INV_COSTS,     /* [N][L]                                          */
+  SCG_SLAB_BACKLOG_COSTS, /* [N][L]                                          */
+  SCG_SLAB_TERMINAL_OBS,  /* [N][L]                                          */
+  SCG_SLAB_RING,          /* [R][N][L]                                       */
+  SCG_SLAB_EPISODE_RETURN,/* int64 [N] (word offset, 8-byte aligned)         */
+  SCG_SLAB_FINAL_RETURN,  /* int64 [N]                                       */
+  SCG_SLAB_HISTORY,       /* [T+1][N][L] when requested, else == total       */
+  SCG_SLAB_TOTAL,         /* words in the slab                               */
+  SCG_SLAB_FIELDS
+};
+
+/*
+ * STREAM copy of `bytes` (a multiple of 16, 16-byte aligned DEVICE buffers) with `blocks`
+ * workgroups of 256 lanes: the achievable-HBM-bandwidth probe bench.py reports beside the
+ * 8 TB/s spec (roofline.measured_peak). Not part of the env path.
+ */
+SCG_API int scg_stream_copy(const void* src, void* dst, int64_t bytes, int32_t blocks, void* stream);
 
 /* ABI version (SCG_ABI_VERSION of the built library). */
 SCG_API int scg_abi_version(void);
@@ -147,6 +184,15 @@ SCG_API int scg_poisson_table(double lam, uint32_t* out, int32_t cap);
  */
 SCG_API int scg_bg_prepare(scg_bg_config* cfg);
 
+/*
+ * Word offsets of one state slab for n_envs envs of a prepared cfg (ring_slots known),
+ * with the order history when with_history != 0. Host only; the caller allocates
+ * offsets[SCG_SLAB_TOTAL] int32 words of DEVICE memory (16-byte aligned, zeroed), points
+ * the scg_bg_state buffers at base + offsets[field] and sets st->slab = base.
+ */
+SCG_API int scg_bg_slab_layout(const scg_bg_config* cfg, int64_t n_envs, int32_t with_history,
+                               int64_t offsets[SCG_SLAB_FIELDS]);
+
 /* reset() for all N envs (beergame_env.py:140-156). obs: DEVICE int32 [N][L] or NULL. */
 SCG_API int scg_bg_reset(const scg_bg_config* cfg, scg_bg_state* st, int32_t* obs, void* stream);
 
@@ -159,6 +205,8 @@ SCG_API int scg_bg_reset(const scg_bg_config* cfg, scg_bg_state* st, int32_t* ob
  *   terminal_obs DEVICE int32 [N][L] or NULL: observation at the terminal week
  * Returns SCG_ERR_PAST_HORIZON when called after the terminal week without auto-reset.
  * Sets *done (host, may be NULL) to 1 when this step was the terminal week (:134).
+ * With st->slab set, reward == obs + N*L (one output allocation) and terminal_obs NULL or the
+ * slab's SCG_SLAB_TERMINAL_OBS view, the slab kernel runs (terminal obs into the slab).
  */
 SCG_API int scg_bg_step(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* action,
                 int32_t* obs, int32_t* reward, int32_t* terminal_obs, uint32_t flags,

@@ -145,3 +145,36 @@ def test_step_rejects_shards_beyond_int32_before_any_launch():
     out = ctypes.c_int32(0)
     rc = nat.lib.scg_bg_step(ctypes.byref(c), ctypes.byref(st), fake, fake, fake, None, 0, ctypes.byref(out), None)
     assert rc == nat.SCG_ERR_INVALID and "n_envs" in nat.last_error()
+
+
+def test_slab_layout():
+    """scg_bg_slab_layout: 16-byte header, six [N][L] rows, the ring, two int64 returns,
+    the optional history; rejects batches whose rows would not stay 16-byte aligned."""
+    import ctypes
+    from gym_supplychain_amd import _native as nat
+    T = 35
+    c = nat.BgConfig()
+    c.levels, c.max_weeks = 4, T
+    d = (ctypes.c_int32 * (T + 1))(*([2] * (T + 1)))
+    dem = (ctypes.c_int32 * T)(*([8] * T))
+    plan = (ctypes.c_int32 * (T + 1))()
+    c.shipment_delays, c.customer_demand = ctypes.cast(d, ctypes.c_void_p), ctypes.cast(dem, ctypes.c_void_p)
+    c.plan = ctypes.cast(plan, ctypes.c_void_p)
+    assert nat.lib.scg_bg_prepare(ctypes.byref(c)) == 0
+    N, L, R = 65536, 4, c.ring_slots
+    assert R == 3
+    off = (ctypes.c_int64 * nat.SLAB_FIELDS)()
+    assert nat.lib.scg_bg_slab_layout(ctypes.byref(c), N, 1, off) == 0
+    NL = N * L
+    assert off[nat.SLAB_ERROR] == 0 and off[nat.SLAB_INVENTORY] == 4
+    assert [off[nat.SLAB_INVENTORY + f] for f in range(6)] == [4 + f * NL for f in range(6)]
+    assert off[nat.SLAB_RING] == 4 + 6 * NL
+    assert off[nat.SLAB_EPISODE_RETURN] == 4 + (6 + R) * NL and off[nat.SLAB_EPISODE_RETURN] % 2 == 0
+    assert off[nat.SLAB_FINAL_RETURN] == off[nat.SLAB_EPISODE_RETURN] + 2 * N
+    assert off[nat.SLAB_HISTORY] == off[nat.SLAB_FINAL_RETURN] + 2 * N
+    assert off[nat.SLAB_TOTAL] == off[nat.SLAB_HISTORY] + (T + 1) * NL
+    assert nat.lib.scg_bg_slab_layout(ctypes.byref(c), N, 0, off) == 0
+    assert off[nat.SLAB_TOTAL] == off[nat.SLAB_HISTORY]
+    assert nat.lib.scg_bg_slab_layout(ctypes.byref(c), 77, 0, off) == 0                     # 77 * 4 % 4 == 0
+    c.levels = 3
+    assert nat.lib.scg_bg_slab_layout(ctypes.byref(c), 77, 0, off) == nat.SCG_ERR_INVALID

@@ -63,11 +63,7 @@ def main():
                         ignore=shutil.ignore_patterns("*.so", "__pycache__"))
     out = os.path.join(pkg, "libscgpu.so")
     srcs = [os.path.join(csrc, s) for s in build_native.SOURCES]
-    cmd = [build_native.hipcc(), f"--offload-arch={build_native.ARCH}"] + build_native.HIP_FLAGS + \
-        ["-I", inc, "-I", csrc, "-O3", "-o", out] + \
-        [f"-D{d}" for d in a.defines] + srcs
-    print("[exp_build]", " ".join(cmd))
-    subprocess.run(cmd, check=True)
+    build_native.compile_library(out, srcs, [inc, csrc], extra=[f"-D{d}" for d in a.defines], verbose=False)
     import sysconfig
     bout = os.path.join(pkg, "_scgpu_fast" + sysconfig.get_config_var("EXT_SUFFIX"))
     subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", sysconfig.get_paths()["include"], "-I", inc,

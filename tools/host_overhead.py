@@ -72,6 +72,16 @@ def main():
     t2 = time.perf_counter()
     out["step_loop"] = (t1 - t0) / a.iters * 1e6
     out["step_loop_wall_us"] = (t2 - t0) / a.iters * 1e6
+    # the C entry point alone, arguments prepared (no Python wrapper): binding + library + HIP launch
+    args = (env._cfg_addr, env._st_addr, week[0].data_ptr(), env._obs_ptr, env._rew_ptr, env._term_ptr, env._flags,
+            nat.raw_stream(0))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        fast(*args)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    out["fast_direct"] = (t1 - t0) / a.iters * 1e6
     ev = [(nat.hip_event(), nat.hip_event()) for _ in range(200)]
     for e in ev:
         env.step(week[env.week], e)
