@@ -343,3 +343,64 @@ def test_auto_kernel_symbols():
     assert env.kernel == "staged" and env.kernel_symbol == "scg::sc_step_staged_kernel<16>"
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, kernel="level")
     assert env.kernel_symbol.startswith("scg::sc_level_kernel<2, ")
+
+
+# ---- full horizon at the BASELINE sizes (configs 3 and 4), into a second episode ---------
+FULL_CASES = {
+    "2perstage": ("sc-2perstage-v0", 65536, {}),
+    "ntom": ("sc-Nperstage-multiproduct-v0", 262144, dict(nodes_per_echelon=[8, 8, 8, 16])),
+    "ntom_stoch": ("sc-Nperstage-multiproduct-v0", 262144,
+                   dict(nodes_per_echelon=[8, 8, 8, 16], stochastic_leadtimes=True, avg_leadtime=2, max_leadtime=4)),
+}
+
+
+@pytest.mark.parametrize("case", sorted(FULL_CASES))
+def test_full_horizon_episode_matches_oracle(case):
+    """A whole 360-step episode at the BASELINE batch size, auto-reset into episode 2 and 3
+    steps of it, with 32 sampled envs (block edges, first and last env included) compared
+    with the oracle at every step: observations, rewards and done exactly, the terminal
+    observation, the reset observation and the episode return. Heaps reach their peak
+    occupancy over a full episode; check_errors() proves no in-transit heap overflowed."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+
+    import gym_supplychain_amd as gsa
+    from sc_replay import replay
+    scenario, N, kw = FULL_CASES[case]
+    seed, extra = 1234, 3
+    env = gsa.make_vec(scenario, N, seed=seed, device=DEV, obs_dtype=torch.float64, auto_reset=True, **kw)
+    sp = env.spec
+    T = sp.total_time_steps
+    sample = sorted({0, 1, 63, 64, 65, 127, 4095, 4096, N // 3, N // 2, N // 2 + 1, N - 65, N - 64, N - 2, N - 1} |
+                    set(range(7, N, N // 17)))[:32]
+    idx = torch.as_tensor(sample, device=DEV)
+    obs0 = env.reset().index_select(0, idx).cpu().numpy()
+    gen = torch.Generator(device=DEV).manual_seed(77)
+    K = T + extra
+    acts = np.zeros((K, len(sample), env.n_actions), dtype=np.float32)
+    obs_rec = np.zeros((K, len(sample), env.n_obs))
+    rew_rec = np.zeros((K, len(sample)))
+    for k in range(K):
+        a = torch.rand((N, env.n_actions), generator=gen, device=DEV, dtype=torch.float32) * 2.2 - 1.1
+        obs, rew, done, info = env.step(a)
+        acts[k] = a.index_select(0, idx).cpu().numpy()
+        shown = info["terminal_observation"] if k == T - 1 else obs
+        obs_rec[k] = shown.index_select(0, idx).cpu().numpy()
+        rew_rec[k] = rew.index_select(0, idx).cpu().numpy()
+        assert bool(done.all()) == (k == T - 1)
+        if k == T - 1:
+            reset_obs = obs.index_select(0, idx).cpu().numpy()
+            final = info["episode_return"].index_select(0, idx).cpu().numpy()
+    env.check_errors()
+    nodes = gsa.envs.scenarios.SCENARIOS[scenario](**kw)[0]
+    okw = dict(num_products=sp.P, demand_range=sp.demand_range, processing_ratio=sp.processing_ratio,
+               stochastic_leadtimes=sp.stochastic_leadtimes, avg_leadtime=sp.avg_leadtime,
+               max_leadtime=sp.max_leadtime, total_time_steps=T, **sp.penalties)
+    jobs = [dict(env=n, nodes=nodes, okw=okw, seed=seed, R=sp.n_retailers, n_lt=sp.n_leadtimes,
+                 lt=(sp.avg_leadtime, sp.max_leadtime), demand_range=sp.demand_range, acts=acts[:, j],
+                 obs=obs_rec[:, j], rew=rew_rec[:, j], first_obs=obs0[j], reset_obs=reset_obs[j],
+                 final_return=float(final[j]), T=T) for j, n in enumerate(sample)]
+    with cf.ProcessPoolExecutor(max_workers=8, mp_context=mp.get_context("spawn")) as pool:
+        results = list(pool.map(replay, jobs))
+    bad = [(n, b) for n, b in results if b]
+    assert not bad, bad[:3]
