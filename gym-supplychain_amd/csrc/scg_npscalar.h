@@ -15,11 +15,15 @@
 
 namespace scg {
 
+// Kind codes form a bit lattice, so NEP 50 promotion is one bitwise OR (np_promote):
+// Python scalars adopt the other side's kind, float32 with float64 or int64 is float64,
+// Python float with int64 is float64. float64 has two codes, 7 and 5 (= PYF | I64); every
+// test below treats them alike, and ABI-facing kinds go through np_kind_abi/np_kind_int.
 enum NpKind : int {
   NK_INT = 0,  // Python int   (weak)
   NK_PYF = 1,  // Python float (weak float64)
-  NK_F32 = 2,  // np.float32
-  NK_F64 = 3,  // np.float64
+  NK_F32 = 3,  // np.float32
+  NK_F64 = 7,  // np.float64 (also 5)
   NK_I64 = 4   // np.int64
 };
 
@@ -31,16 +35,14 @@ struct Num {
 __host__ __device__ __forceinline__ Num pyint(double v) { return Num{v, NK_INT}; }
 __host__ __device__ __forceinline__ Num f64(double v) { return Num{v, NK_F64}; }
 
-// Result kind of a binary arithmetic op (NEP 50: Python scalars adopt the other side's
-// dtype kind when it is a NumPy scalar; int64 with any float is float64). Written as
-// selects, not branches: kinds are per-lane data, and on the GPU a branch on them costs
-// exec-mask bookkeeping even when every lane agrees.
-__host__ __device__ __forceinline__ int np_promote(int a, int b) {
-  const int lo = a < b ? a : b, hi = a < b ? b : a;
-  const int pyf = hi == NK_I64 ? NK_F64 : hi;
-  const int r = lo == NK_INT ? hi : (lo == NK_PYF ? pyf : NK_F64);
-  return a == b ? a : r;
-}
+// Result kind of a binary arithmetic op. A select-free OR: kinds are per-lane data, and on
+// the GPU every select or branch on them is an instruction in each scalar operation.
+__host__ __device__ __forceinline__ int np_promote(int a, int b) { return a | b; }
+
+// The ABI's kind numbering (scgpu.h ledger_kind: 0 int, 1 float, 2 float32, 3 float64,
+// 4 int64) to and from the lattice codes.
+__host__ __device__ __forceinline__ int np_kind_abi(int k) { return k == NK_F32 ? 2 : ((k & 5) == 5 ? 3 : k); }
+__host__ __device__ __forceinline__ int np_kind_int(int a) { return a == 2 ? NK_F32 : (a == 3 ? NK_F64 : a); }
 
 // float32 rounding of an operation whose NumPy result kind is float32: operands are cast
 // to float32 (exact for float32 values, round-to-nearest for Python scalars), then the
@@ -66,11 +68,10 @@ __host__ __device__ __forceinline__ Num np_mul(Num a, Num b) {
   return Num{k == NK_F32 ? r32 : r64, k};
 }
 
-// True division: int/int -> Python float, int64/int -> float64.
+// True division: int/int -> Python float, int64/int -> float64: the kind OR 1 (0 -> 1,
+// 4 -> 5; float kinds keep theirs).
 __host__ __device__ __forceinline__ Num np_div(Num a, Num b) {
-  int k = np_promote(a.k, b.k);
-  if (k == NK_INT) k = NK_PYF;
-  if (k == NK_I64) k = NK_F64;
+  const int k = np_promote(a.k, b.k) | NK_PYF;
   if (k == NK_F32) return Num{static_cast<double>(static_cast<float>(a.v) / static_cast<float>(b.v)), k};
   return Num{a.v / b.v, k};
 }
@@ -78,10 +79,9 @@ __host__ __device__ __forceinline__ Num np_div(Num a, Num b) {
 __host__ __device__ __forceinline__ Num np_neg(Num a) { return Num{-a.v, a.k}; }
 
 // Comparisons: a float32 against a Python scalar compares in float32 (the Python value
-// is cast); every other pairing compares the exact values.
-__host__ __device__ __forceinline__ bool np_f32_cmp(const Num& a, const Num& b) {
-  return (a.k == NK_F32 && (b.k == NK_INT || b.k == NK_PYF)) || (b.k == NK_F32 && (a.k == NK_INT || a.k == NK_PYF));
-}
+// is cast); every other pairing compares the exact values. Two float32 values compare the
+// same either way (both exact in a double), so "the kinds OR to float32" is the test.
+__host__ __device__ __forceinline__ bool np_f32_cmp(const Num& a, const Num& b) { return (a.k | b.k) == NK_F32; }
 
 __host__ __device__ __forceinline__ bool np_lt(Num a, Num b) {
   const bool c32 = static_cast<float>(a.v) < static_cast<float>(b.v);

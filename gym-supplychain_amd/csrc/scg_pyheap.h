@@ -26,13 +26,13 @@ __host__ __device__ __forceinline__ int32_t he_time(int32_t tk) { return tk >> 3
 __host__ __device__ __forceinline__ int he_kind(int32_t tk) { return tk & 7; }
 __host__ __device__ __forceinline__ int32_t he_pack(int32_t time, int kind) { return (time << 3) | kind; }
 
-// Python tuple (t1, a1) < (t2, a2)
+// Python tuple (t1, a1) < (t2, a2): times first; on equal times the amounts (equal amounts
+// are not less, and np_lt already says so). Evaluated without branches: inside a sift loop
+// each early return was a divergent branch with its exec-mask bookkeeping.
 __host__ __device__ __forceinline__ bool he_less(const HeapEntry& x, const HeapEntry& y) {
   const int32_t tx = he_time(x.tk), ty = he_time(y.tk);
-  if (tx != ty) return tx < ty;
   const Num ax{x.v, he_kind(x.tk)}, ay{y.v, he_kind(y.tk)};
-  if (np_eq(ax, ay)) return false;
-  return np_lt(ax, ay);
+  return (tx < ty) | ((tx == ty) & np_lt(ax, ay));
 }
 
 struct HeapView {

@@ -135,36 +135,39 @@ __global__ __launch_bounds__(kScBlock) void sc_step_kernel(const ScArgs a) {
   if (e.overflow) atomicOr(a.err, 1);
 }
 
-// The same step with this block's 64 env heaps staged in LDS: heap pushes/pops/walks are
+// The same step with this block's EPB env heaps staged in LDS: heap pushes/pops/walks are
 // chains of dependent accesses, so they run at LDS latency instead of L2/HBM latency.
 // Layout [slot][lane] (lane fastest): any mix of per-lane heap positions is bank-conflict
 // free. Stock stays in HBM (a few accesses per node). Rows are staged in and out with
-// coalesced 64-lane transfers, copying only the live entries (< heap size) of each lane.
-template <int MAXD>
-__global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
+// coalesced transfers, copying only the live entries (< heap size) of each lane.
+// EPB (envs = threads per block) is 64, or 32 when the batch is too small to give every
+// SIMD two full waves: a step is one long dependent chain per lane, and at one wave per
+// SIMD nothing hides its latency, so two half-full waves finish sooner than one full one.
+template <int MAXD, int EPB>
+__global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x;
-  const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + lane;
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * EPB + lane;
   const ScCtx& c = a.c;
   const int NP = c.n_nodes * c.P;
   const int slots = NP * c.H;
   double* lval = reinterpret_cast<double*>(smem);
-  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
-  int32_t* lsize = ltk + static_cast<int64_t>(slots) * kScBlock;
+  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * EPB);
+  int32_t* lsize = ltk + static_cast<int64_t>(slots) * EPB;
   const bool live = n < a.n;
   if (live) {
     for (int hp = 0; hp < NP; ++hp) {
       const int32_t sz = a.size[hp * a.n + n];
-      lsize[hp * kScBlock + lane] = sz;
+      lsize[hp * EPB + lane] = sz;
       for (int j = 0; j < sz; ++j) {
         const int64_t g = (static_cast<int64_t>(hp) * c.H + j) * a.n + n;
-        ltk[(hp * c.H + j) * kScBlock + lane] = a.tk[g];
-        lval[(hp * c.H + j) * kScBlock + lane] = a.val[g];
+        ltk[(hp * c.H + j) * EPB + lane] = a.tk[g];
+        lval[(hp * c.H + j) * EPB + lane] = a.val[g];
       }
     }
   }
   if (!live) return;  // no block-wide sync below: every lane only touches its own column
-  ScEnv e{a.stock + n, ltk + lane, lval + lane, lsize + lane, a.n, kScBlock,
+  ScEnv e{a.stock + n, ltk + lane, lval + lane, lsize + lane, a.n, EPB,
           static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
   if (a.led_v) {
     e.led_v = a.led_v + n;
@@ -199,12 +202,12 @@ __global__ __launch_bounds__(kScBlock) void sc_step_lds_kernel(const ScArgs a) {
   }
   if (e.overflow) atomicOr(a.err, 1);
   for (int hp = 0; hp < NP; ++hp) {
-    const int32_t sz = lsize[hp * kScBlock + lane];
+    const int32_t sz = lsize[hp * EPB + lane];
     a.size[hp * a.n + n] = sz;
     for (int j = 0; j < sz; ++j) {
       const int64_t g = (static_cast<int64_t>(hp) * c.H + j) * a.n + n;
-      a.tk[g] = ltk[(hp * c.H + j) * kScBlock + lane];
-      a.val[g] = lval[(hp * c.H + j) * kScBlock + lane];
+      a.tk[g] = ltk[(hp * c.H + j) * EPB + lane];
+      a.val[g] = lval[(hp * c.H + j) * EPB + lane];
     }
   }
 }
@@ -521,9 +524,24 @@ bool sc_level_schedule(scg_sc_config* cfg, const scg_sc_node* nodes) {
 // Heaps and sizes only: staging stock and action rows as well (+12 B per heap, +4 B per
 // action) costs sc-2perstage-v0 a block per CU (3 instead of 4 at 65,536 envs), which
 // measured 127 us against 70 us per step on MI355X (profiles/r01f_sc_variants.log).
-size_t sc_lds_bytes(const scg_sc_config* cfg) {
+size_t sc_lds_bytes(const scg_sc_config* cfg, int epb = kScBlock) {
   const size_t NP = static_cast<size_t>(cfg->n_nodes) * cfg->n_products;
-  return kScBlock * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
+  return epb * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
+}
+
+// Envs per block of the LDS lane kernel for a batch of n: half-full waves when full ones
+// would leave a SIMD with fewer than two (the CU count is read once per device).
+#ifndef SCG_SC_LDS_EPB
+#define SCG_SC_LDS_EPB 0  // 0 = by batch size; 32 or 64 forces one
+#endif
+int sc_lds_epb(int64_t n) {
+  if (SCG_SC_LDS_EPB) return SCG_SC_LDS_EPB;
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus[dev] = 256;
+  return n < static_cast<int64_t>(cus[dev]) * 4 * 2 * 64 ? 32 : 64;
 }
 // Staged kernel: one heap per lane.
 size_t sc_staged_lds_bytes(const scg_sc_config* cfg) {
@@ -765,13 +783,22 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
   } else if (cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST) {
     return fail(SCG_ERR_INVALID, "lane kernel needs the env-fastest layout");
   } else if (lds <= kScLdsMax) {
+    const int epb = sc_lds_epb(st->n_envs);
+    const dim3 g2(static_cast<unsigned>((st->n_envs + epb - 1) / epb));
+    const size_t l2 = sc_lds_bytes(cfg, epb);
+#define SCG_LDS_LAUNCH(D)                                                                     \
+  if (epb == 32)                                                                              \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_lds_kernel<D, 32>), g2, dim3(32), l2, s, a);   \
+  else                                                                                        \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_lds_kernel<D, 64>), g2, dim3(64), l2, s, a)
     switch (sc_maxd_bucket(cfg->max_dests)) {
-      case 2: hipLaunchKernelGGL(sc_step_lds_kernel<2>, grid, dim3(kScBlock), lds, s, a); break;
-      case 4: hipLaunchKernelGGL(sc_step_lds_kernel<4>, grid, dim3(kScBlock), lds, s, a); break;
-      case 8: hipLaunchKernelGGL(sc_step_lds_kernel<8>, grid, dim3(kScBlock), lds, s, a); break;
-      case 16: hipLaunchKernelGGL(sc_step_lds_kernel<16>, grid, dim3(kScBlock), lds, s, a); break;
-      default: hipLaunchKernelGGL(sc_step_lds_kernel<32>, grid, dim3(kScBlock), lds, s, a); break;
+      case 2: SCG_LDS_LAUNCH(2); break;
+      case 4: SCG_LDS_LAUNCH(4); break;
+      case 8: SCG_LDS_LAUNCH(8); break;
+      case 16: SCG_LDS_LAUNCH(16); break;
+      default: SCG_LDS_LAUNCH(32); break;
     }
+#undef SCG_LDS_LAUNCH
   } else switch (sc_maxd_bucket(cfg->max_dests)) {
     case 2: hipLaunchKernelGGL(sc_step_kernel<2>, grid, dim3(kScBlock), 0, s, a); break;
     case 4: hipLaunchKernelGGL(sc_step_kernel<4>, grid, dim3(kScBlock), 0, s, a); break;

@@ -94,12 +94,12 @@ __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int k
   if (!e.led_v) return;
   const int64_t i0 = (static_cast<int64_t>(key) * c.P + p) * e.led_stride;
   const int64_t i1 = (static_cast<int64_t>(SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride;
-  const Num a = np_add(Num{e.led_v[i0], e.led_k[i0]}, cost);
-  const Num b = np_add(Num{e.led_v[i1], e.led_k[i1]}, units);
+  const Num a = np_add(Num{e.led_v[i0], np_kind_int(e.led_k[i0])}, cost);
+  const Num b = np_add(Num{e.led_v[i1], np_kind_int(e.led_k[i1])}, units);
   e.led_v[i0] = a.v;
-  e.led_k[i0] = a.k;
+  e.led_k[i0] = np_kind_abi(a.k);
   e.led_v[i1] = b.v;
-  e.led_k[i1] = b.k;
+  e.led_k[i1] = np_kind_abi(b.k);
 }
 
 // est_episode at reset (:684-695): every entry the Python int 0
@@ -107,7 +107,7 @@ __host__ __device__ inline void sc_reset_ledger(const ScCtx& c, ScEnv& e) {
   if (!e.led_v) return;
   for (int q = 0; q < 2 * SCG_SC_LEDGER_KEYS * c.P; ++q) {
     e.led_v[q * e.led_stride] = 0.0;
-    e.led_k[q * e.led_stride] = NK_INT;
+    e.led_k[q * e.led_stride] = np_kind_abi(NK_INT);
   }
 }
 

@@ -460,7 +460,13 @@ class SupplyChainVecEnv:
         if self.kernel == "staged":
             return f"scg::sc_step_staged_kernel<{maxd}>"
         lds = 64 * len(self.spec.nodes) * self.spec.P * (12 * c.heap_capacity + 4)
-        return f"scg::sc_step_lds_kernel<{maxd}>" if lds <= 64 * 1024 else f"scg::sc_step_kernel<{maxd}>"
+        if lds > 64 * 1024:
+            return f"scg::sc_step_kernel<{maxd}>"
+        # envs per block as scg_supplychain.hip sc_lds_epb picks them: half-full waves when
+        # full ones would give a SIMD fewer than two
+        cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        epb = 32 if self.n_envs < cus * 4 * 2 * 64 else 64
+        return f"scg::sc_step_lds_kernel<{maxd}, {epb}>"
 
     def check_errors(self):
         """Raise if any env's in-transit heap overflowed its capacity (never expected: the

@@ -338,7 +338,10 @@ def test_auto_kernel_symbols():
     node-staged kernel (config 4); kernel_symbol names what rocprofv3 reports."""
     import gym_supplychain_amd as gsa
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV)
-    assert env.kernel == "lane" and env.kernel_symbol == "scg::sc_step_lds_kernel<2>"
+    assert env.kernel == "lane" and env.kernel_symbol == "scg::sc_step_lds_kernel<2, 32>"
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    env = gsa.make_vec("sc-2perstage-v0", cus * 512, device=DEV)
+    assert env.kernel_symbol == "scg::sc_step_lds_kernel<2, 64>"
     env = gsa.make_vec("sc-Nperstage-multiproduct-v0", 64, device=DEV, nodes_per_echelon=[8, 8, 8, 16])
     assert env.kernel == "staged" and env.kernel_symbol == "scg::sc_step_staged_kernel<16>"
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, kernel="level")
@@ -404,3 +407,26 @@ def test_full_horizon_episode_matches_oracle(case):
         results = list(pool.map(replay, jobs))
     bad = [(n, b) for n, b in results if b]
     assert not bad, bad[:3]
+
+
+def test_lds_kernel_block_sizes_agree():
+    """The LDS lane kernel runs 32 envs per block below two full waves per SIMD and 64 above
+    (scg_supplychain.hip sc_lds_epb); an env's trajectory depends only on its global id, so
+    the first envs of a small batch and of a large one must match bit for bit over a whole
+    episode and into the next."""
+    import gym_supplychain_amd as gsa
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    n_small, n_big = 1000, cus * 512 + 1000
+    small = gsa.make_vec("sc-2perstage-v0", n_small, seed=5, device=DEV, obs_dtype=torch.float64, auto_reset=True)
+    big = gsa.make_vec("sc-2perstage-v0", n_big, seed=5, device=DEV, obs_dtype=torch.float64, auto_reset=True)
+    assert small.kernel_symbol.endswith(", 32>") and big.kernel_symbol.endswith(", 64>")
+    o1, o2 = small.reset(), big.reset()
+    assert torch.equal(o1, o2[:n_small])
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    for t in range(small.spec.total_time_steps + 5):
+        a = torch.rand((n_big, big.n_actions), generator=gen, device=DEV) * 2 - 1
+        o1, r1, d1, _ = small.step(a[:n_small].contiguous())
+        o2, r2, d2, _ = big.step(a)
+        assert torch.equal(o1, o2[:n_small]) and torch.equal(r1, r2[:n_small]), t
+    small.check_errors()
+    big.check_errors()

@@ -1,6 +1,7 @@
 """Build experiment variants of libscgpu.so side by side (for A/B timing on the GPU box).
 
     python tools/exp_build.py NAME [--rev GIT_REV] [--file csrc/X.h=REV ...] [-D MACRO=V ...]
+                              [--replace csrc/X.h OLD NEW ...]
 
 Writes exp/NAME/gym_supplychain_amd/ — a copy of the package whose libscgpu.so is built
 from the working-tree csrc/ (or from GIT_REV, or per-file revisions) with extra -D flags.
@@ -30,6 +31,8 @@ def main():
     ap.add_argument("--rev", default=None, help="take every csrc file and include/scgpu.h from this revision")
     ap.add_argument("--file", action="append", default=[], help="csrc/FILE=REV: one file from a revision")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--replace", nargs=3, action="append", default=[], metavar=("FILE", "OLD", "NEW"),
+                    help="csrc/FILE: replace the exact text OLD by NEW (it must occur); for ablations")
     a = ap.parse_args()
     root = os.path.join(REPO, "exp", a.name)
     shutil.rmtree(root, ignore_errors=True)
@@ -49,6 +52,13 @@ def main():
     for spec in a.file:
         path, rev = spec.split("=")
         open(os.path.join(csrc, os.path.basename(path)), "w").write(git_show(rev, f"gym-supplychain_amd/{path}"))
+    for f, old, new in a.replace:
+        path = os.path.join(csrc, os.path.basename(f))
+        text = open(path).read()
+        old, new = old.encode().decode("unicode_escape"), new.encode().decode("unicode_escape")
+        if old not in text:
+            sys.exit(f"--replace: text not found in {f}: {old!r}")
+        open(path, "w").write(text.replace(old, new))
     pkg = os.path.join(root, "gym_supplychain_amd")
     if a.rev:  # the Python package of that revision too (it must match the library's ABI)
         files = subprocess.run(["git", "-C", REPO, "ls-tree", "-r", "--name-only", a.rev,
