@@ -15,6 +15,56 @@
 #include <vector>
 
 #include "scg_common.h"
+
+// Diagnostic build only (-DSCG_SC_STAMPS, tools/sc_stamps.py): lane 0 of every wave of the
+// LDS lane kernel records the shader clock at phase boundaries into a buffer of its own
+// (g_sc_stamps, read back by scg_sc_debug_stamps); nothing else reads it. 0 start, 1 heaps
+// staged, 2.. after each node's act (node i at 2 + min(i, 20)), 23 return, 24 observation,
+// 25 heaps stored. In the product build SCG_STAMP is empty.
+#ifdef SCG_SC_STAMPS
+constexpr int kStampSlots = 32;
+constexpr int kStampWaves = 1 << 16;
+__device__ unsigned long long g_sc_stamps[kStampWaves * kStampSlots];
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SCG_STAMP(k)                                                                                  \
+  do {                                                                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                                     \
+    const unsigned w_ = blockIdx.x * ((blockDim.x + 63u) / 64u) + threadIdx.x / 64u;                 \
+    if ((threadIdx.x & 63u) == 0 && w_ < static_cast<unsigned>(kStampWaves)) g_sc_stamps[w_ * kStampSlots + (k)] = now_; \
+  } while (0)
+namespace scg {
+struct ScAcc {
+  unsigned long long a[16];
+  unsigned long long last;
+};
+}  // namespace scg
+#define SCG_ACC_DECL scg::ScAcc scg_acc_{{0}, __builtin_amdgcn_s_memtime()};
+#define SCG_ACCP(ptr, k)                                           \
+  do {                                                             \
+    if (ptr) {                                                     \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+      (ptr)->a[k] += now_ - (ptr)->last;                           \
+      (ptr)->last = now_;                                          \
+    }                                                              \
+  } while (0)
+#define SCG_ACC(k)                                               \
+  do {                                                           \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    scg_acc_.a[k] += now_ - scg_acc_.last;                       \
+    scg_acc_.last = now_;                                        \
+  } while (0)
+#define SCG_ACC_STORE                                                                             \
+  do {                                                                                            \
+    const unsigned w_ = blockIdx.x * ((blockDim.x + 63u) / 64u) + threadIdx.x / 64u;             \
+    if ((threadIdx.x & 63u) == 0 && w_ < static_cast<unsigned>(kStampWaves))                      \
+      for (int k_ = 0; k_ < 16; ++k_) g_sc_stamps[w_ * kStampSlots + 16 + k_] = scg_acc_.a[k_];          \
+  } while (0)
+#endif
+#endif
+
+#ifndef SCG_SC_LDS_PROBE
+#define SCG_SC_LDS_PROBE 0
+#endif
 #include "scg_supplychain_core.h"
 #include "scg_supplychain_level.h"
 #include "scg_supplychain_staged.h"
@@ -151,6 +201,7 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
   const ScCtx& c = a.c;
   const int NP = c.n_nodes * c.P;
   const int slots = NP * c.H;
+  SCG_STAMP(0);
   double* lval = reinterpret_cast<double*>(smem);
   int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * EPB);
   int32_t* lsize = ltk + static_cast<int64_t>(slots) * EPB;
@@ -166,15 +217,31 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
       }
     }
   }
+#if SCG_SC_LDS_PROBE
+  double* lstock = reinterpret_cast<double*>(lsize + NP * EPB);
+  float* lact = reinterpret_cast<float*>(lstock + NP * EPB);
+  if (live) {
+    for (int k = 0; k < NP; ++k) lstock[k * EPB + lane] = a.stock[k * a.n + n];
+    for (int k = 0; k < c.A; ++k) lact[lane * c.A + k] = a.act[n * c.A + k];
+  }
+  const float* act_row = lact + lane * c.A;
+  double* stock_col = lstock + lane;
+  const int64_t stock_stride = EPB;
+#else
+  const float* act_row = a.act + n * c.A;
+  double* stock_col = a.stock + n;
+  const int64_t stock_stride = a.n;
+#endif
+  SCG_STAMP(1);
   if (!live) return;  // no block-wide sync below: every lane only touches its own column
-  ScEnv e{a.stock + n, ltk + lane, lval + lane, lsize + lane, a.n, EPB,
+  ScEnv e{stock_col, ltk + lane, lval + lane, lsize + lane, stock_stride, EPB,
           static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
   if (a.led_v) {
     e.led_v = a.led_v + n;
     e.led_k = a.led_k + n;
     e.led_stride = a.n;
   }
-  const double reward = sc_step_env<MAXD>(c, e, a.act + n * c.A, a.t);
+  const double reward = sc_step_env<MAXD>(c, e, act_row, a.t);
   a.rew[n] = reward;
   const bool terminal = a.flags & 1;
   if (a.ep_ret) {
@@ -182,6 +249,7 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
     if (terminal && a.final_ret) a.final_ret[n] = r;
     a.ep_ret[n] = (a.flags & 2) ? 0.0 : r;
   }
+  SCG_STAMP(23);
   if (a.flags & 2) {
     if (a.term_obs) {
       ObsRow tout{a.term_obs, n * c.O, a.obs_f64};
@@ -200,6 +268,10 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
       sc_observe(c, e, a.t, tout);
     }
   }
+  SCG_STAMP(24);
+#if SCG_SC_LDS_PROBE
+  for (int k = 0; k < NP; ++k) a.stock[k * a.n + n] = lstock[k * EPB + lane];
+#endif
   if (e.overflow) atomicOr(a.err, 1);
   for (int hp = 0; hp < NP; ++hp) {
     const int32_t sz = lsize[hp * EPB + lane];
@@ -210,6 +282,7 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
       a.val[g] = lval[(hp * c.H + j) * EPB + lane];
     }
   }
+  SCG_STAMP(25);
 }
 
 // Node-staged step (scg_supplychain_staged.h): one lane per env; the heap being worked on
@@ -224,10 +297,11 @@ __global__ __launch_bounds__(kScBlock) void sc_step_staged_kernel(const ScArgs a
   if (n >= a.n) return;
   const ScCtx& c = a.c;
   double* lval = reinterpret_cast<double*>(smem);
-  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(c.H) * kScBlock);
+  const int slots = c.H > MAXD ? c.H : MAXD;  // sc_staged_lds_bytes
+  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
   ScEnv g = env_view(a, n, a.episode);
   const HeapView lh{ltk + lane, lval + lane, kScBlock};
-  const StagedInbox in{a.inbox_tk + n, a.inbox_val + n, a.n};
+  const StagedInbox in{a.inbox_tk + n, a.inbox_val + n, a.n, lh};
   const bool terminal = a.flags & 1;
   const bool autoreset = a.flags & 2;
   // node observations go to obs, or to the terminal observation when the env resets now
@@ -526,7 +600,8 @@ bool sc_level_schedule(scg_sc_config* cfg, const scg_sc_node* nodes) {
 // measured 127 us against 70 us per step on MI355X (profiles/r01f_sc_variants.log).
 size_t sc_lds_bytes(const scg_sc_config* cfg, int epb = kScBlock) {
   const size_t NP = static_cast<size_t>(cfg->n_nodes) * cfg->n_products;
-  return epb * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4);
+  return epb * NP * (static_cast<size_t>(cfg->heap_capacity) * 12 + 4) +
+         (SCG_SC_LDS_PROBE ? epb * (NP * 8 + static_cast<size_t>(cfg->n_actions) * 4) : 0);
 }
 
 // Envs per block of the LDS lane kernel for a batch of n: half-full waves when full ones
@@ -543,9 +618,9 @@ int sc_lds_epb(int64_t n) {
     cus[dev] = 256;
   return n < static_cast<int64_t>(cus[dev]) * 4 * 2 * 64 ? 32 : 64;
 }
-// Staged kernel: one heap per lane.
+// Staged kernel: one heap per lane, or the split's scratch (sc_split_scratch) when wider.
 size_t sc_staged_lds_bytes(const scg_sc_config* cfg) {
-  return kScBlock * static_cast<size_t>(cfg->heap_capacity) * 12;
+  return kScBlock * static_cast<size_t>(std::max(cfg->heap_capacity, sc_maxd_bucket(cfg->max_dests))) * 12;
 }
 
 // The staged kernel's inbox (scg_supplychain_staged.h): every shipment must go to a later
@@ -816,6 +891,17 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
   if (done) *done = terminal ? 1 : 0;
   return SCG_OK;
 }
+
+#ifdef SCG_SC_STAMPS
+// Diagnostic build only: copy the phase stamps of the first `waves` waves to host memory.
+__attribute__((visibility("default"))) int scg_sc_debug_stamps(unsigned long long* host, int waves) {
+  if (waves > kStampWaves) waves = kStampWaves;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(SCG_ERR_HIP, "sync");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sc_stamps), sizeof(unsigned long long) * kStampSlots * waves) != hipSuccess)
+    return fail(SCG_ERR_HIP, "stamp copy");
+  return SCG_OK;
+}
+#endif
 
 int scg_sc_draw_tables(const scg_sc_config* cfg, const scg_sc_state* st, uint32_t episode, int32_t* demand,
                        int32_t* leadtimes, void* stream) {

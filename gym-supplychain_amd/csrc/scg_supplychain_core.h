@@ -17,6 +17,20 @@
 #include "scg_pyheap.h"
 #include "scgpu.h"
 
+// Diagnostic phase stamps (SCG_SC_STAMPS builds only, scg_supplychain.hip): no-ops here.
+// SCG_STAMP(k) records the clock in slot k; SCG_ACC(k) adds the cycles since the previous
+// SCG_ACC to accumulator k (declared by SCG_ACC_DECL, stored by SCG_ACC_STORE).
+#ifndef SCG_STAMP
+#define SCG_STAMP(k)
+#define SCG_ACC_DECL scg::ScAcc scg_acc_{};
+#define SCG_ACC(k)
+#define SCG_ACC_STORE
+#define SCG_ACCP(ptr, k)
+namespace scg {
+struct ScAcc {};
+}
+#endif
+
 namespace scg {
 
 // Compile-time destination bound used for a chain whose widest node ships to d nodes.
@@ -78,6 +92,7 @@ struct ScEnv {
   int32_t* led_k = nullptr;
   int64_t led_stride = 0;
   int32_t hnode0 = 0;  // first node whose heaps the heap arrays hold (staged kernel: the current one)
+  ScAcc* dbg = nullptr;  // diagnostic builds only (SCG_ACCP)
 };
 
 // info['sc_episode'] categories in the reference's dict order (:416-417)
@@ -217,6 +232,8 @@ __host__ __device__ __forceinline__ void sc_push(const ScCtx& c, ScEnv& e, int n
 // destination does; a heap push keeps the loop rolled to bound code size).
 struct DirectPush {
   static constexpr bool kUnroll = false;
+  static constexpr bool kLdsSplit = false;  // see sc_split_scratch
+  __host__ __device__ Num scratch_get(int) const { return pyint(0); }
   __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv& e, int /*src*/, int /*d*/, int dest, int p,
                                                 int32_t time, Num amount) const {
     sc_push(c, e, dest, p, time, amount);
@@ -277,41 +294,96 @@ struct NumVec {
 // SC_Action.apply for SHIP (:58-96): the cut [0, limit] split at the destinations'
 // sorted action values; amount_i = (v_(k) - v_(k-1)) * limit, clamped to what is left.
 // Sorting (value, index) tuples is done by ranks so every array index is a compile-time
-// constant (MAXD-unrolled loops): the arrays stay in registers instead of scratch.
-template <int MAXD>
+// constant (MAXD-unrolled loops): the arrays stay in registers instead of scratch. K <= MAXD
+// bounds the loops (a node with D <= K destinations runs the K-sized split; D is uniform).
+template <int MAXD, int K = MAXD>
 __host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num limit, NumVec<MAXD>& out) {
 #pragma unroll
   for (int i = 0; i < MAXD; ++i) out.set(i, pyint(0));
   Num left = limit;
   if (!np_lt(pyint(0), left)) return;
-  int rank[MAXD];
+  // rank[i] = #{j : (vals[j], j) < (vals[i], i)}, each pair compared once
+  int rank[K];
 #pragma unroll
-  for (int i = 0; i < MAXD; ++i) {
-    int r = 0;
+  for (int i = 0; i < K; ++i) rank[i] = 0;
 #pragma unroll
-    for (int j = 0; j < MAXD; ++j)
-      if (j < D && (vals[j] < vals[i] || (vals[j] == vals[i] && j < i))) ++r;
-    rank[i] = r;
-  }
+  for (int i = 0; i < K; ++i)
+#pragma unroll
+    for (int j = i + 1; j < K; ++j)
+      if (j < D) {
+        const bool j_first = vals[j] < vals[i];  // on a tie the lower index i comes first
+        rank[i] += j_first ? 1 : 0;
+        rank[j] += j_first ? 0 : 1;
+      }
   float prev = 0.0f;
   bool first = true;  // the first cut starts at the Python int 0
 #pragma unroll
-  for (int s = 0; s < MAXD; ++s) {
+  for (int s = 0; s < K; ++s) {
     if (s >= D) continue;
     float v = 0.0f;
 #pragma unroll
-    for (int i = 0; i < MAXD; ++i)
+    for (int i = 0; i < K; ++i)
       if (i < D && rank[i] == s) v = vals[i];
     const Num diff = first ? np_sub(Num{v, NK_F32}, pyint(0)) : np_sub(Num{v, NK_F32}, Num{prev, NK_F32});
     Num amt = np_mul(diff, limit);
     if (np_lt(left, amt)) amt = left;
 #pragma unroll
-    for (int i = 0; i < MAXD; ++i)
+    for (int i = 0; i < K; ++i)
       if (i < D && rank[i] == s) out.set(i, amt);
     left = np_sub(left, amt);
     prev = v;
     first = false;
   }
+}
+
+// The same split with its working arrays in per-lane scratch slots (the staged kernel's
+// heap staging area, free while a node acts): each value is written to the slot of its
+// rank, the cut is walked in slot order, and amount s is left in slot s, where destination
+// i reads it at rank[i] — no O(D^2) selects and no per-destination amount registers.
+// Returns false when nothing is cut (limit <= 0: every amount is the Python int 0).
+template <int MAXD, class Scratch>
+__host__ __device__ inline bool sc_split_scratch(const float (&vals)[MAXD], int D, Num limit, const Scratch& scr,
+                                                 int (&rank)[MAXD]) {
+  Num left = limit;
+  if (!np_lt(pyint(0), left)) return false;
+#pragma unroll
+  for (int i = 0; i < MAXD; ++i) rank[i] = 0;
+#pragma unroll
+  for (int i = 0; i < MAXD; ++i)
+#pragma unroll
+    for (int j = i + 1; j < MAXD; ++j)
+      if (j < D) {
+        const bool j_first = vals[j] < vals[i];  // on a tie the lower index i comes first
+        rank[i] += j_first ? 1 : 0;
+        rank[j] += j_first ? 0 : 1;
+      }
+#pragma unroll
+  for (int i = 0; i < MAXD; ++i)
+    if (i < D) scr.scratch_put_value(rank[i], vals[i]);
+  float prev = 0.0f;
+  for (int s = 0; s < D; ++s) {
+    const float v = scr.scratch_value(s);
+    const Num diff = s == 0 ? np_sub(Num{v, NK_F32}, pyint(0)) : np_sub(Num{v, NK_F32}, Num{prev, NK_F32});
+    Num amt = np_mul(diff, limit);
+    if (np_lt(left, amt)) amt = left;
+    scr.scratch_put(s, amt);
+    left = np_sub(left, amt);
+    prev = v;
+  }
+  return true;
+}
+
+// The split sized to the node: chains mixing narrow and wide nodes (ntom: 8 and 16
+// destinations) run the narrow nodes' O(D^2) ranking at their own size.
+template <int MAXD>
+__host__ __device__ __forceinline__ void sc_split_d(const float (&vals)[MAXD], int D, Num limit, NumVec<MAXD>& out) {
+  if constexpr (MAXD > 8) {
+    if (D <= 8) {
+      sc_split<MAXD, 8>(vals, D, limit, out);
+      return;
+    }
+  }
+  sc_split<MAXD>(vals, D, limit, out);
 }
 
 // Action k of this env, denormalised like _denormalize_action (:697-698): (a + 1) / 2 on
@@ -373,6 +445,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
       sc_note(c, e, LK_SUPPLY, p, cst, amount);
     }
   }
+  SCG_ACCP(e.dbg, 8);
   if (!nd.last_level) {
     // SHIP (:262-375)
     const int D = nd.n_dests;
@@ -389,9 +462,16 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
       if (np_lt(pyint(0), material)) {
         float vals[MAXD];
         NumVec<MAXD> out;
+        int rank[MAXD];
+        bool cut = false;  // kLdsSplit: the split's amounts are in the scratch slots
 #pragma unroll
         for (int i = 0; i < MAXD; ++i) vals[i] = i < D ? static_cast<float>(sc_action(act, nd.action_offset + a_i + i).v) : 0.0f;
-        sc_split<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), out);
+        if constexpr (Push::kLdsSplit) {
+          cut = sc_split_scratch<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), push, rank);
+        } else {
+          sc_split_d<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), out);
+        }
+        SCG_ACCP(e.dbg, 9);
         // The reference's per-destination passes — processing capacity and ratio
         // (:298-310), ship capacity (:312-328), sum(amounts) (:331), the pushes (:344-348)
         // and sum(calculate_costs(amounts_to_ship)) (:352) — each carry their own
@@ -401,7 +481,11 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         // per-destination array besides the split's output stays live.
         Num leaving = pyint(0), ship_cost = pyint(0), ship_units = pyint(0);
         auto dest_step = [&](int i) {
-          Num o = out.get_dyn(i);
+          Num o;
+          if constexpr (Push::kLdsSplit)
+            o = cut ? push.scratch_get(rank[i]) : pyint(0);
+          else
+            o = out.get_dyn(i);
           Num snt = o;  // amounts_to_ship = amounts.copy() (:292)
           if (factory) {
             if (np_lt(pyint(0), o)) {
@@ -433,8 +517,9 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         } else {
           for (int i = 0; i < D; ++i) dest_step(i);
         }
-        double& st = sc_stock(c, e, ni, p);
-        st = st - leaving.v;  // float64 array element minus the promoted scalar (:332)
+        SCG_ACCP(e.dbg, 10);
+        // float64 array element minus the promoted scalar (:332); nothing above wrote it
+        sc_stock(c, e, ni, p) = material.v - leaving.v;
         if (factory) {
           const Num proc = np_mul(leaving, pyint(nd.processing_cost[p]));
           cost = np_add(cost, proc);
@@ -464,6 +549,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
       sc_note(c, e, LK_UNMET, p, pen, unmet);
     }
   }
+  SCG_ACCP(e.dbg, 11);
   for (int p = 0; p < P; ++p) {  // holding (:390-394)
     const Num held = f64(sc_stock(c, e, ni, p));
     const Num hold = np_mul(held, pyint(nd.stock_cost[p]));
@@ -479,7 +565,10 @@ template <int MAXD>
 __host__ __device__ inline double sc_step_env(const ScCtx& c, ScEnv& e, const float* act, int t) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   Num total = pyint(0);
-  for (int i = 0; i < c.n_nodes; ++i) total = np_add(total, sc_node_act<MAXD>(c, e, ltc, dmc, i, act, t));
+  for (int i = 0; i < c.n_nodes; ++i) {
+    total = np_add(total, sc_node_act<MAXD>(c, e, ltc, dmc, i, act, t));
+    SCG_STAMP(2 + (i < 20 ? i : 20));
+  }
   return np_neg(total).v;
 }
 

@@ -41,6 +41,8 @@ struct LevelInbox {
   int32_t src0, dst0, wsrc, wdst;
 
   static constexpr bool kUnroll = true;  // an LDS store per destination
+  static constexpr bool kLdsSplit = false;
+  __host__ __device__ Num scratch_get(int) const { return pyint(0); }
   __host__ __device__ __forceinline__ void ship(const ScCtx&, ScEnv&, int src, int /*d*/, int dest, int p, int32_t time,
                                                 Num amount) const {
     const int idx = (p * wsrc + (src - src0)) * wdst + (dest - dst0);

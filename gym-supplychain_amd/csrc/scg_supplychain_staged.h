@@ -28,13 +28,37 @@
 
 namespace scg {
 
+__host__ __device__ __forceinline__ int32_t sc_f2i(float f) {
+  int32_t i;
+  __builtin_memcpy(&i, &f, sizeof(i));
+  return i;
+}
+__host__ __device__ __forceinline__ float sc_i2f(int32_t i) {
+  float f;
+  __builtin_memcpy(&f, &i, sizeof(f));
+  return f;
+}
+
 // Shipments into the destinations' inbox entries; entry q of this env at [q * stride].
 struct StagedInbox {
   int32_t* tk;  // time << 3 | kind, -1 = no shipment
   double* val;
   int64_t stride;
+  HeapView scr;  // the heap staging area, scratch for sc_split_scratch while a node acts
 
   static constexpr bool kUnroll = true;  // a store per destination
+  static constexpr bool kLdsSplit = true;
+  __host__ __device__ __forceinline__ void scratch_put_value(int s, float v) const {
+    scr.tk[s * scr.stride] = sc_f2i(v);
+  }
+  __host__ __device__ __forceinline__ float scratch_value(int s) const { return sc_i2f(scr.tk[s * scr.stride]); }
+  __host__ __device__ __forceinline__ void scratch_put(int s, Num x) const {
+    scr.tk[s * scr.stride] = x.k;
+    scr.val[s * scr.stride] = x.v;
+  }
+  __host__ __device__ __forceinline__ Num scratch_get(int s) const {
+    return Num{scr.val[s * scr.stride], scr.tk[s * scr.stride]};
+  }
   __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv&, int src, int d, int /*dest*/, int p,
                                                 int32_t time, Num amount) const {
     ScNode& nd = c.nodes[src];
@@ -59,7 +83,7 @@ struct StagedInbox {
 template <class Sink>
 __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
                                                WordCache& ltc, const float* act, int t, int i, int p, int& a_i,
-                                               int& lt_i, Sink& out) {
+                                               int& lt_i, Sink& out, ScAcc& scg_acc_) {
   ScNode& nd = c.nodes[i];
   const HeapView gh = sc_heap(c, g, i, p);
   int32_t& gsz = sc_size(c, g, i, p);
@@ -76,6 +100,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
   for (int u = 0; u < kChunk; ++u)
     if (u < nd.in_deg) ib[u] = HeapEntry{in.tk[(q0 + u) * in.stride], in.val[(q0 + u) * in.stride]};
   int32_t sz = gsz;
+  SCG_ACC(7);
   for (int j0 = 0; j0 < sz; j0 += kChunk) {
     HeapEntry b[kChunk];
 #pragma unroll
@@ -85,6 +110,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
     for (int u = 0; u < kChunk; ++u)
       if (j0 + u < sz) lh.put(j0 + u, b[u]);
   }
+  SCG_ACC(0);
   for (int k0 = 0; k0 < nd.in_deg; k0 += kChunk) {
     if (k0 > 0) {
 #pragma unroll
@@ -96,7 +122,9 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
     for (int u = 0; u < kChunk; ++u)  // in source order (:347)
       if (k0 + u < nd.in_deg && ib[u].tk >= 0 && !py_heappush(lh, sz, c.H, ib[u])) g.overflow = 1;
   }
+  SCG_ACC(1);
   st = st0 + sc_receive(lh, sz, t);
+  SCG_ACC(2);
   if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) {
     const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));
     ++a_i;
@@ -106,8 +134,10 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
       ++lt_i;
     }
   }
+  SCG_ACC(3);
   sc_observe_bins(c, lh, sz, t, i, p, out, [&](int k, const HeapEntry& e) { gh.put(k, e); });  // copy back
   gsz = sz;
+  SCG_ACC(4);
 }
 
 // SupplyChainEnv.step body (:704-738) plus the node part of _build_observation (:762-791)
@@ -122,14 +152,22 @@ __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const
                                                  const float* act, int t, Sink& out) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   Num total = pyint(0);
+  SCG_ACC_DECL
+#ifdef SCG_SC_STAMPS
+  g.dbg = &scg_acc_;
+#endif
   for (int i = 0; i < c.n_nodes; ++i) {
     ScNode& nd = c.nodes[i];
     int a_i = 0, lt_i = 0;
-    for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out);
+    for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out, scg_acc_);
     if (!nd.last_level) in.clear(c, i);
+    SCG_ACC(7);
     total = np_add(total, sc_node_act<MAXD, StagedInbox, true>(c, g, ltc, dmc, i, act, t, in));
+    SCG_ACC(5);
     for (int p = 0; p < c.P; ++p) sc_observe_stock(c, g, i, p, out);
+    SCG_ACC(6);
   }
+  SCG_ACC_STORE;
   return np_neg(total).v;
 }
 

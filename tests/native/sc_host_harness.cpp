@@ -4,6 +4,7 @@
 // product: libscgpu.so has no CPU path, and this library is built by the tests only.
 #include <cstring>
 
+#include <algorithm>
 #include <vector>
 
 #include "scg_supplychain_core.h"
@@ -88,10 +89,11 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
     }
     const float* a = actions + static_cast<int64_t>(t - 1) * c.A;
     if (mode == 2) {  // sc_step_staged_kernel: one node's heaps staged, shipments via the inbox
-      std::vector<int32_t> ltk(c.H, 0x7fffffff), inbox_tk(cfg->inbox_size > 0 ? cfg->inbox_size : 1, 0x7fffffff);
-      std::vector<double> lval(c.H, -1.0), inbox_val(inbox_tk.size(), -1.0);
+      const int slots = std::max(c.H, scg::sc_maxd_bucket(cfg->max_dests));  // heap or split scratch
+      std::vector<int32_t> ltk(slots, 0x7fffffff), inbox_tk(cfg->inbox_size > 0 ? cfg->inbox_size : 1, 0x7fffffff);
+      std::vector<double> lval(slots, -1.0), inbox_val(inbox_tk.size(), -1.0);
       const scg::HeapView loc{ltk.data(), lval.data(), 1};
-      const scg::StagedInbox in{inbox_tk.data(), inbox_val.data(), 1};
+      const scg::StagedInbox in{inbox_tk.data(), inbox_val.data(), 1, loc};
       double* row = obs + static_cast<int64_t>(t) * c.O;
       auto out = [row](int o, double v) { row[o] = v; };
       double r = 0.0;

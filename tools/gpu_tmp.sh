@@ -1,1 +1,5 @@
-SC_NO_PMC=1 bash tools/gpu_sc_ab.sh c epb64 abl_split abl_dest abl_obs wpe3 wpe4 && timeout -k 10 600 python -u -m pytest tests/test_gpu_supplychain.py -x -q --timeout 300 --timeout-method thread > gpurun_out/sc_c/pytest_sc.log 2>&1; echo "pytest rc=$?"; tail -3 gpurun_out/sc_c/pytest_sc.log
+SC_NO_PMC=1 bash tools/gpu_sc_ab.sh f chunk8 chunk16
+cd gpurun_out/sc_f && for f in bench_*.log; do echo "$f"; grep '^{' $f | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print('   ', d['config']['kernel'], d['config']['n_envs'], round(d['roofline']['avg_kernel_us'],1), 'us', round(d['roofline']['frac'],3))"; done
