@@ -66,9 +66,14 @@ def compile_library(out, srcs, include_dirs, extra=(), opt="-O3", verbose=True):
     os.makedirs(objdir, exist_ok=True)
     inc = [x for d in include_dirs for x in ("-I", d)]
     objs = [os.path.join(objdir, os.path.splitext(os.path.basename(s))[0] + ".o") for s in srcs]
+    # an object is reused when it is newer than its source, every header and this script
+    hdr = [os.path.join(d, f) for d in include_dirs for f in os.listdir(d) if f.endswith(".h")]
+    newest_dep = max([os.path.getmtime(h) for h in hdr] + [os.path.getmtime(__file__)])
 
     def cc(src_obj):
         src, obj = src_obj
+        if os.path.exists(obj) and os.path.getmtime(obj) >= max(newest_dep, os.path.getmtime(src)):
+            return
         cmd = [hipcc(), f"--offload-arch={ARCH}"] + HIP_FLAGS + inc + [opt, *extra, "-c", src, "-o", obj]
         if verbose:
             print("[build_native]", " ".join(cmd), flush=True)
@@ -81,7 +86,6 @@ def compile_library(out, srcs, include_dirs, extra=(), opt="-O3", verbose=True):
         print("[build_native]", " ".join(link), flush=True)
     subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
-    shutil.rmtree(objdir, ignore_errors=True)
     return out
 
 

@@ -457,6 +457,11 @@ int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, int32_t 
                      int32_t lo, int32_t hi, int32_t* out, void* stream) {
   if (!out || n_envs <= 0 || rows <= 0 || width <= 0 || hi < lo)
     return fail(SCG_ERR_INVALID, "bad uniform_ints arguments");
+  // The Philox env counter is 32-bit: global env ids past 2^32 would reuse another env's draws.
+  if (env_offset < 0 || env_offset + n_envs > (int64_t(1) << 32))
+    return fail(SCG_ERR_INVALID, "uniform_ints env ids must lie in [0, 2^32)");
+  if (static_cast<int64_t>(rows) * width > INT32_MAX)
+    return fail(SCG_ERR_INVALID, "uniform_ints rows * width must fit int32");
   const uint32_t range = static_cast<uint32_t>(static_cast<int64_t>(hi) - lo + 1);  // 0 means 2^32
   if (range == 0) return fail(SCG_ERR_INVALID, "uniform_ints range must be < 2^32");
   hipLaunchKernelGGL(uniform_ints_kernel, grid_for(n_envs), dim3(kBlock), 0, static_cast<hipStream_t>(stream),

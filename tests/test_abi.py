@@ -147,6 +147,19 @@ def test_step_rejects_shards_beyond_int32_before_any_launch():
     assert rc == nat.SCG_ERR_INVALID and "n_envs" in nat.last_error()
 
 
+def test_uniform_ints_rejects_env_ids_and_sizes_before_any_launch():
+    """scg_uniform_ints: the Philox env counter is 32-bit and the per-env word count int32, so
+    ids past 2^32 and rows*width past INT32_MAX are rejected before any HIP call."""
+    from gym_supplychain_amd import _native as nat
+    fake = ctypes.c_void_p(0x1000)  # never dereferenced
+    rc = nat.lib.scg_uniform_ints(1, 2 ** 32 - 4, 8, 1, 4, 0, 0, 9, fake, None)
+    assert rc == nat.SCG_ERR_INVALID and "2^32" in nat.last_error()
+    rc = nat.lib.scg_uniform_ints(1, -1, 8, 1, 4, 0, 0, 9, fake, None)
+    assert rc == nat.SCG_ERR_INVALID
+    rc = nat.lib.scg_uniform_ints(1, 0, 8, 65536, 65536, 0, 0, 9, fake, None)
+    assert rc == nat.SCG_ERR_INVALID and "int32" in nat.last_error()
+
+
 def test_slab_layout():
     """scg_bg_slab_layout: 16-byte header, six [N][L] rows, the ring, two int64 returns,
     the optional history; rejects batches whose rows would not stay 16-byte aligned."""
