@@ -13,7 +13,9 @@ async RCCL all-gather of per-env episode returns at each episode end.
 
 Timing (rank 0 prints ONE JSON line):
   * warm-up: max(W, 35) untimed steps — at least one whole 35-week episode, so every week
-    kind of the plan and the auto-reset have run before timing ("warmup_steps_run");
+    kind of the plan and the auto-reset have run before timing — then one untimed region of
+    the timed region's shape (synchronize, K steps, synchronize); "warmup_steps_run" counts
+    both. The collector is off from there on;
   * the timed region is exactly K steps, bracketed by barrier + synchronize, max over
     ranks; `value` = envs of all ranks x K / that wall time. Nothing inside is stamped
     except the first and the last launch, whose own dispatch begin / end timestamps
@@ -280,6 +282,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=1.5)
     ap.add_argument("--kernel-samples", type=int, default=350,
                     help="launches timed one at a time with kernel-stamped events after the timed region")
+    ap.add_argument("--no-dry-region", action="store_true",
+                    help="skip the untimed K-step region (sync, K steps, sync) run right before the timed one")
     args = ap.parse_args()
 
     import torch
@@ -328,6 +332,11 @@ def main():
 
     warmup_run = max(args.warmup, WEEKS)
     loop.run(warmup_run)
+    if not args.no_dry_region:  # one untimed region of the same shape (sync, K steps, sync) right
+        region(loop, args.steps, world, barrier, sync)  # before: 7.9e9-9.8e9 -> 1.01e10-1.04e10 at K = 20
+        warmup_run += args.steps                        # (profiles/r02m_dry_region.log)
+    import gc
+    gc.disable()  # no collector pass inside a timed region
     # headline: exactly K steps
     timed_bytes = bytes_of(args.steps)
     elapsed, gpu_ms = region(loop, args.steps, world, barrier, sync, (ev[0], ev[1], nat.hip_event_elapsed_ms))
