@@ -15,7 +15,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "gym_supplychain_amd", "libscgpu.so")
 SOURCES = ["scg_common.hip", "scg_beergame.hip", "scg_bg_levels_1.hip", "scg_bg_levels_2.hip", "scg_bg_levels_3.hip",
-           "scg_bg_levels_4.hip", "scg_supplychain.hip"]
+           "scg_bg_levels_4.hip", "scg_supplychain.hip", "scg_sc_nodes.hip"]
 ARCH = "gfx950"
 
 

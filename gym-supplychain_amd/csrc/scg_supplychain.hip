@@ -66,77 +66,19 @@ struct ScAcc {
 #define SCG_SC_LDS_PROBE 0
 #endif
 #include "scg_supplychain_core.h"
+#include "scg_supplychain_args.h"
 #include "scg_supplychain_level.h"
 #include "scg_supplychain_staged.h"
 #include "scgpu.h"
 
 namespace scg {
 
-constexpr int kScBlock = 64;
-
-struct ScArgs {
-  ScCtx c;
-  double* stock;
-  int32_t* tk;
-  double* val;
-  int32_t* size;
-  const float* act;
-  void* obs;
-  void* term_obs;
-  double* rew;
-  double* ep_ret;
-  double* final_ret;
-  int32_t* err;
-  int32_t* inbox_tk;  // staged kernel: shipment inbox [inbox_size][N]
-  double* inbox_val;
-  double* led_v;     // build_info ledgers [2*8*P][N] (lane kernels) or null
-  int32_t* led_k;
-  double* led_fv;    // terminal-step ledger on auto-reset
-  int32_t* led_fk;
-  int64_t n;
-  int64_t env_offset;
-  uint32_t episode;
-  int32_t t;       // the step being simulated (1..T) / 0 for reset
-  int32_t flags;   // bit0 terminal, bit1 autoreset
-  int32_t obs_f64;
-  int32_t layout;  // SCG_SC_LAYOUT_*
-};
-
-struct ObsRow {
-  void* base;
-  int64_t row;
-  int f64;
-  __device__ __forceinline__ void operator()(int o, double x) const {
-    if (f64)
-      static_cast<double*>(base)[row + o] = x;
-    else
-      static_cast<float*>(base)[row + o] = static_cast<float>(x);
-  }
-};
-
-__device__ __forceinline__ ScEnv env_view(const ScArgs& a, int64_t n, uint32_t episode) {
-  if (a.layout == SCG_SC_LAYOUT_ENV_MAJOR) {  // env n's block: [NP], [NP][H]
-    const int64_t NP = static_cast<int64_t>(a.c.n_nodes) * a.c.P;
-    return ScEnv{a.stock + n * NP, a.tk + n * NP * a.c.H, a.val + n * NP * a.c.H, a.size + n * NP, 1, 1,
-                 static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
-  }
-  ScEnv e{a.stock + n, a.tk + n, a.val + n, a.size + n, a.n, a.n, static_cast<uint32_t>(a.env_offset + n), n, episode, 0};
-  if (a.led_v) {
-    e.led_v = a.led_v + n;
-    e.led_k = a.led_k + n;
-    e.led_stride = a.n;
-  }
-  return e;
-}
-
-// Auto-reset keeps the finished episode's ledger (the info of the terminal step, :744-746).
-__device__ __forceinline__ void snapshot_ledger(const ScArgs& a, const ScCtx& c, int64_t n) {
-  if (!a.led_v || !a.led_fv) return;
-  for (int q = 0; q < 2 * SCG_SC_LEDGER_KEYS * c.P; ++q) {
-    a.led_fv[q * a.n + n] = a.led_v[q * a.n + n];
-    a.led_fk[q * a.n + n] = a.led_k[q * a.n + n];
-  }
-}
+// scg_sc_nodes.hip
+size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W);
+int sc_nodes_waves(int n_nodes);
+int sc_nodes_max_dests();
+size_t sc_nodes_lds_max();
+int sc_launch_nodes(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t s);
 
 __global__ __launch_bounds__(kScBlock) void sc_reset_kernel(const ScArgs a) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
@@ -155,34 +97,7 @@ template <int MAXD>
 __global__ __launch_bounds__(kScBlock) void sc_step_kernel(const ScArgs a) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
   if (n >= a.n) return;
-  ScEnv e = env_view(a, n, a.episode);
-  const double reward = sc_step_env<MAXD>(a.c, e, a.act + n * a.c.A, a.t);
-  a.rew[n] = reward;
-  const bool terminal = a.flags & 1;
-  if (a.ep_ret) {
-    const double r = a.ep_ret[n] + reward;  // episode_rewards += current_reward (:739)
-    if (terminal && a.final_ret) a.final_ret[n] = r;
-    a.ep_ret[n] = (a.flags & 2) ? 0.0 : r;
-  }
-  if (a.flags & 2) {  // auto-reset: terminal observation aside, fresh episode in place
-    if (a.term_obs) {
-      ObsRow tout{a.term_obs, n * a.c.O, a.obs_f64};
-      sc_observe(a.c, e, a.t, tout);
-    }
-    snapshot_ledger(a, a.c, n);
-    e.episode = a.episode + 1;
-    sc_reset_env(a.c, e);
-    ObsRow out{a.obs, n * a.c.O, a.obs_f64};
-    sc_observe(a.c, e, 0, out);
-  } else {
-    ObsRow out{a.obs, n * a.c.O, a.obs_f64};
-    sc_observe(a.c, e, a.t, out);
-    if (terminal && a.term_obs) {
-      ObsRow tout{a.term_obs, n * a.c.O, a.obs_f64};
-      sc_observe(a.c, e, a.t, tout);
-    }
-  }
-  if (e.overflow) atomicOr(a.err, 1);
+  sc_lane_step<MAXD>(a, n);
 }
 
 // The same step with this block's EPB env heaps staged in LDS: heap pushes/pops/walks are
@@ -758,7 +673,7 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   // reference's chains as measured on MI355X)
   int want = cfg->kernel;
   if (want != SCG_SC_KERNEL_AUTO && want != SCG_SC_KERNEL_LANE && want != SCG_SC_KERNEL_LEVEL &&
-      want != SCG_SC_KERNEL_STAGED)
+      want != SCG_SC_KERNEL_STAGED && want != SCG_SC_KERNEL_NODES)
     return fail(SCG_ERR_INVALID, "kernel=%d is not a SCG_SC_KERNEL_* value", want);
   cfg->n_levels = 0;
   cfg->group = 1;
@@ -770,6 +685,22 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   if (want == SCG_SC_KERNEL_AUTO && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
     std::vector<scg_sc_node> probe(nodes, nodes + NN);
     if (sc_inbox_layout(cfg, probe.data()) >= 0) want = SCG_SC_KERNEL_STAGED;
+  }
+  if (want == SCG_SC_KERNEL_NODES) {
+    const int entries = sc_inbox_layout(cfg, nodes);
+    if (entries < 0)
+      return fail(SCG_ERR_INVALID, "the node-parallel kernel needs every shipment to go to a later node, once per list");
+    const int W = sc_nodes_waves(NN);
+    if (maxd > sc_nodes_max_dests())
+      return fail(SCG_ERR_INVALID, "the node-parallel kernel takes nodes with at most %d destinations", sc_nodes_max_dests());
+    if (H > 64 || sc_nodes_lds_bytes(NN, P, H, entries, W) > sc_nodes_lds_max())
+      return fail(SCG_ERR_INVALID, "a block's heaps and inbox (%d nodes x %d products x %d slots, %d entries) exceed "
+                  "the node-parallel kernel's LDS", NN, P, H, entries);
+    cfg->inbox_size = entries;
+    cfg->group = W;
+    cfg->kernel = SCG_SC_KERNEL_NODES;
+    cfg->layout = SCG_SC_LAYOUT_ENV_FASTEST;
+    return SCG_OK;
   }
   if (want == SCG_SC_KERNEL_STAGED) {
     const int entries = sc_inbox_layout(cfg, nodes);
@@ -817,7 +748,7 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
   a.term_obs = terminal_obs;
   a.rew = reward;
   a.t = t;
-  a.flags = (terminal ? 1 : 0) | (autoreset ? 2 : 0);
+  a.flags = (terminal ? 1 : 0) | (autoreset ? 2 : 0) | ((flags & SCG_SC_SERIAL) ? 4 : 0);
   const dim3 grid = sc_grid(st->n_envs);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t lds = sc_lds_bytes(cfg);
@@ -844,6 +775,10 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
       default: SCG_LEVEL_LAUNCH(32); break;
     }
 #undef SCG_LEVEL_LAUNCH
+  } else if (cfg->kernel == SCG_SC_KERNEL_NODES && !st->ledger) {
+    if (cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST || cfg->inbox_size < 0)
+      return fail(SCG_ERR_INVALID, "node-parallel kernel needs the layout and inbox scg_sc_prepare derives");
+    if (int rc = sc_launch_nodes(a, sc_maxd_bucket(cfg->max_dests), cfg->group, cfg->inbox_size, s)) return rc;
   } else if (cfg->kernel == SCG_SC_KERNEL_STAGED) {
     if (!st->inbox_tk || !st->inbox_val || cfg->inbox_size < 0)
       return fail(SCG_ERR_INVALID, "the staged kernel needs the inbox buffers [inbox_size][N]");

@@ -30,6 +30,7 @@ SCG_DEMAND_POISSON = 2
 SCG_DEMAND_UNIFORM = 3
 
 SCG_BG_AUTORESET = 1
+SCG_SC_SERIAL = 2  # node-parallel SupplyChain kernel: every env through its serial walk (tests)
 SCG_STREAM_DEMAND = 0
 SCG_STREAM_ACTION = 1
 SCG_STREAM_BG2_DEMAND = 4
@@ -111,7 +112,7 @@ SC_MAX_NODES = 256
 SC_MAX_LEVELS = 16
 SC_LEDGER_KEYS = 8  # info["sc_episode"] categories (supplychain_env.py:416-417)
 SC_LEDGER_NAMES = ("stock", "stock_pen", "supply", "process", "process_pen", "ship", "ship_pen", "unmet_dem")
-SC_KERNEL_AUTO, SC_KERNEL_LANE, SC_KERNEL_LEVEL, SC_KERNEL_STAGED = 0, 1, 2, 3
+SC_KERNEL_AUTO, SC_KERNEL_LANE, SC_KERNEL_LEVEL, SC_KERNEL_STAGED, SC_KERNEL_NODES = 0, 1, 2, 3, 4
 SC_LAYOUT_ENV_FASTEST, SC_LAYOUT_ENV_MAJOR = 0, 1
 SCG_STREAM_SC_DEMAND = 2
 SCG_STREAM_SC_LEADTIME = 3

@@ -218,9 +218,11 @@ class SupplyChainVecEnv:
     [N, T, n_lt] used for every episode instead of the Philox draws (e.g. to replay the
     reference's RandomState episodes exactly).
     kernel: "auto" / "lane" (one lane walks one env's whole chain), "level" (a lane group
-    per env, one lane per node of a level) or "staged" (one lane per env, the current
-    node's heaps in LDS, shipments through an HBM inbox); DESIGN.md §6. All give the same
-    results; the state layout follows the kernel.
+    per env, one lane per node of a level), "staged" (one lane per env, the current
+    node's heaps in LDS, shipments through an HBM inbox) or "nodes" (a wave per node of 64
+    envs, every node acting at once, heaps and shipments in LDS; with build_info the lane
+    kernel runs instead); DESIGN.md §6. All give the same results; the state layout follows
+    the kernel.
     spec.build_info: every step's info holds 'sc_episode' = {'rewards': [N], 'costs':
     {key: [N, P]}, 'units': {key: [N, P]}} (device views, float64; the NumPy type of every
     entry in ledger_kinds()), the reference's episode ledgers (:684-695, :750-760); with
@@ -229,7 +231,7 @@ class SupplyChainVecEnv:
     """
 
     _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL,
-                "staged": nat.SC_KERNEL_STAGED}
+                "staged": nat.SC_KERNEL_STAGED, "nodes": nat.SC_KERNEL_NODES}
 
     def __init__(self, n_envs, nodes_info=None, spec=None, seed=0, device=None, env_offset=0, auto_reset=True,
                  obs_dtype=torch.float32, track_returns=True, demand_table=None, leadtime_table=None, kernel="auto",
@@ -276,7 +278,8 @@ class SupplyChainVecEnv:
         if spec.build_info and c.kernel == nat.SC_KERNEL_LEVEL:
             raise ValueError("build_info ledgers are kept by the lane and staged kernels (kernel='lane', 'staged' or 'auto')")
         nat.check(nat.lib.scg_sc_prepare(ctypes.byref(c), host_nodes))
-        self.kernel = {nat.SC_KERNEL_LEVEL: "level", nat.SC_KERNEL_STAGED: "staged"}.get(c.kernel, "lane")
+        self.kernel = {nat.SC_KERNEL_LEVEL: "level", nat.SC_KERNEL_STAGED: "staged",
+                       nat.SC_KERNEL_NODES: "nodes"}.get(c.kernel, "lane")
         self._env_major = c.layout == nat.SC_LAYOUT_ENV_MAJOR
         if (c.n_actions, c.n_obs, c.n_leadtimes) != (spec.n_actions, spec.n_obs, spec.n_leadtimes):
             raise RuntimeError("host/library disagree on the chain's action/observation sizes")
@@ -459,6 +462,8 @@ class SupplyChainVecEnv:
             return f"scg::sc_level_kernel<{maxd}, {'true' if c.level_staged else 'false'}>"
         if self.kernel == "staged":
             return f"scg::sc_step_staged_kernel<{maxd}>"
+        if self.kernel == "nodes" and not self.spec.build_info:
+            return f"scg::sc_step_nodes_kernel<{maxd}>"
         lds = 64 * len(self.spec.nodes) * self.spec.P * (12 * c.heap_capacity + 4)
         if lds > 64 * 1024:
             return f"scg::sc_step_kernel<{maxd}>"

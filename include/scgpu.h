@@ -67,6 +67,8 @@ typedef enum scg_demand_mode {
 
 /* Step flags */
 #define SCG_BG_AUTORESET 1u /* at the terminal week reset in the same launch (VecEnv semantics) */
+#define SCG_SC_SERIAL 2u    /* node-parallel SupplyChain kernel: step every env with its serial
+                               walk (the path of envs whose receive order it cannot prove; tests) */
 
 /* Philox streams (counter word 3) */
 #define SCG_STREAM_DEMAND 0u
@@ -273,6 +275,8 @@ SCG_API int scg_uniform_ints(uint64_t seed, int64_t env_offset, int64_t n_envs, 
 #define SCG_SC_KERNEL_LEVEL 2 /* a lane group per env, one lane per node of a level; env-major */
 #define SCG_SC_KERNEL_STAGED 3 /* one lane per env, one node's heaps in LDS at a time, shipments
                                   through a per-env global inbox; env-fastest                 */
+#define SCG_SC_KERNEL_NODES 4  /* 64 envs x W waves per block, a wave per node: all nodes act at
+                                  once, heaps and shipments in LDS; env-fastest               */
 #define SCG_SC_LAYOUT_ENV_FASTEST 0 /* stock [NP][N], heaps [NP][H][N], sizes [NP][N]          */
 #define SCG_SC_LAYOUT_ENV_MAJOR 1   /* stock [N][NP], heaps [N][NP][H], sizes [N][NP]          */
 #define SCG_STREAM_SC_DEMAND 2u
@@ -336,10 +340,10 @@ typedef struct scg_sc_config {
    * the next one, so a level's nodes never depend on each other within a step). */
   int32_t kernel;
   int32_t layout;               /* out: SCG_SC_LAYOUT_*                                     */
-  int32_t group;                /* out: lanes per env (level kernel)                        */
+  int32_t group;                /* out: lanes per env (level kernel), waves per block (nodes)*/
   int32_t n_levels;             /* out: 0 when the chain has no such schedule               */
   int32_t level_start[SCG_SC_MAX_LEVELS + 1];
-  int32_t inbox_size;           /* out: shipment inbox entries per env (level kernel)       */
+  int32_t inbox_size;           /* out: shipment inbox entries per env (level/staged/nodes) */
   int32_t level_staged;         /* out: 1 = the level kernel stages each env's state in LDS */
   /* Per-product demand models (demands_generator.py:3-89). demand_models = 0: every
    * product is uniform on [demand_lo, demand_hi]. Otherwise per product p: kind

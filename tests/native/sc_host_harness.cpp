@@ -9,6 +9,7 @@
 
 #include "scg_supplychain_core.h"
 #include "scg_supplychain_level.h"
+#include "scg_supplychain_nodes.h"
 #include "scg_supplychain_staged.h"
 
 namespace {
@@ -22,6 +23,8 @@ struct HostSched {
   }
 };
 }  // namespace
+
+static int nodes_fallbacks = 0;  // node-parallel steps that took the one-lane walk
 
 static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
                         uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
@@ -114,6 +117,59 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
       if (et.overflow) return 1;
       continue;
     }
+    if (mode == 3 || mode == 4) {  // sc_step_nodes_kernel's phases (4: its serial walk every step); nodes in REVERSE order (they are independent)
+      const int E = cfg->inbox_size > 0 ? cfg->inbox_size : 1;
+      std::vector<int32_t> htk(static_cast<size_t>(NP) * c.H, 0x7fffffff), hsz(NP, -1), ibtk(E, 0x7fffffff);
+      std::vector<double> hval(htk.size(), -1.0), recv(NP, -1.0), ibval(E, -1.0);
+      std::vector<scg::Num> cost(c.n_nodes);
+      auto lheap = [&](int hp) { return scg::HeapView{htk.data() + hp * c.H, hval.data() + hp * c.H, 1}; };
+      bool flagged = false;
+      for (int i = c.n_nodes - 1; i >= 0; --i)
+        for (int p = 0; p < c.P; ++p)
+          flagged |= !scg::sc_nodes_stage(c, et, lheap(i * c.P + p), hsz[i * c.P + p], t, i, p, recv[i * c.P + p]);
+      double* row = obs + static_cast<int64_t>(t) * c.O;
+      auto out = [row](int o, double v) { row[o] = v; };
+      const scg::NodesInbox in{ibtk.data(), ibval.data(), 1};
+      if (flagged || mode == 4) {  // the kernel's serial walk on the staged heaps for this env
+        nodes_fallbacks += flagged ? 1 : 0;
+        double r = 0.0;
+        switch (scg::sc_maxd_bucket(cfg->max_dests)) {
+          case 2: r = scg::sc_nodes_serial<2>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          case 4: r = scg::sc_nodes_serial<4>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          case 8: r = scg::sc_nodes_serial<8>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          case 16: r = scg::sc_nodes_serial<16>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          default: r = scg::sc_nodes_serial<32>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+        }
+        rewards[t - 1] = r;
+        for (int k = 0; k < c.R * c.P; ++k) scg::sc_observe_demand(c, et, t, k, out);
+        scg::sc_observe_tail(c, t, out);
+        if (et.overflow) return 1;
+        continue;
+      }
+      for (int i = c.n_nodes - 1; i >= 0; --i) {
+        switch (scg::sc_maxd_bucket(cfg->max_dests)) {
+          case 2: cost[i] = scg::sc_nodes_act<2>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          case 4: cost[i] = scg::sc_nodes_act<4>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          case 8: cost[i] = scg::sc_nodes_act<8>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          case 16: cost[i] = scg::sc_nodes_act<16>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          default: cost[i] = scg::sc_nodes_act<32>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+        }
+        for (int p = 0; p < c.P; ++p) scg::sc_observe_stock(c, et, i, p, out);
+      }
+      for (int i = c.n_nodes - 1; i >= 0; --i) {
+        scg::WordCache ltc{0, scg::U4{0, 0, 0, 0}, false};
+        int a_i = 0, lt_i = 0;
+        for (int p = 0; p < c.P; ++p)
+          scg::sc_nodes_heap(c, et, lheap(i * c.P + p), hsz[i * c.P + p], in, ltc, a, t, i, p, a_i, lt_i, out);
+      }
+      scg::Num total = scg::pyint(0);
+      for (int i = 0; i < c.n_nodes; ++i) total = scg::np_add(total, cost[i]);
+      rewards[t - 1] = scg::np_neg(total).v;
+      for (int k = 0; k < c.R * c.P; ++k) scg::sc_observe_demand(c, et, t, k, out);
+      scg::sc_observe_tail(c, t, out);
+      if (et.overflow) return 1;
+      continue;
+    }
     if (mode == 1) {  // sc_level_kernel's phases, lanes in turn
       scg::ScLevels lv;
       lv.n = cfg->n_levels;
@@ -186,4 +242,34 @@ extern "C" int sch_episode_ledger(const scg_sc_config* cfg, const scg_sc_node* n
                                   double* heap_val, int32_t* heap_size, double* ledger, int32_t* ledger_kind) {
   return episode_impl(0, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
                       heap_val, heap_size, ledger, ledger_kind);
+}
+
+extern "C" int sch_episode_nodes(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                                 uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps, const float* actions,
+                                 double* obs, double* rewards, double* stock, int32_t* heap_tk, double* heap_val,
+                                 int32_t* heap_size) {
+  return episode_impl(3, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+                      heap_val, heap_size);
+}
+
+extern "C" int sch_episode_nodes_serial(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                                        uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps,
+                                        const float* actions, double* obs, double* rewards, double* stock,
+                                        int32_t* heap_tk, double* heap_val, int32_t* heap_size) {
+  return episode_impl(4, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
+                      heap_val, heap_size);
+}
+
+// Steps the node-parallel emulation handed to the one-lane walk since the last call.
+extern "C" int sch_nodes_fallbacks() {
+  const int k = nodes_fallbacks;
+  nodes_fallbacks = 0;
+  return k;
+}
+
+// sc_recv_scan over one heap given as (time<<3|kind, amount) arrays.
+extern "C" int sch_recv_scan(const int32_t* tk, const double* val, int sz, int t, double* recv) {
+  std::vector<int32_t> k(tk, tk + sz);
+  std::vector<double> v(val, val + sz);
+  return scg::sc_recv_scan(scg::HeapView{k.data(), v.data(), 1}, sz, t, *recv) ? 1 : 0;
 }

@@ -26,10 +26,14 @@ def build():
     lib.sch_episode_level.restype = ctypes.c_int
     lib.sch_episode_ledger.restype = ctypes.c_int
     lib.sch_episode_staged.restype = ctypes.c_int
+    lib.sch_episode_nodes.restype = ctypes.c_int
+    lib.sch_nodes_fallbacks.restype = ctypes.c_int
+    lib.sch_episode_nodes_serial.restype = ctypes.c_int
     return lib
 
 
-def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=False, ledger=False, staged=False):
+def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=False, ledger=False, staged=False,
+                nodes_kernel=False, nodes_serial=False):
     """Reset + len(actions) steps of one env; returns obs [T+1, O], rewards [T],
     stock [T+1, NP], heaps (tk, val, size) per snapshot; with ledger=True also the
     build_info ledger after every step (values [T, 2, 8, P], kinds [T, 2, 8, P])."""
@@ -53,6 +57,6 @@ def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=F
         fn = lib.sch_episode_staged if staged else lib.sch_episode_ledger
         rc = fn(*args, p(led_v), p(led_k))
         return rc, obs, rew, stock, (tk, val, size), (led_v, led_k)
-    fn = lib.sch_episode_level if level else lib.sch_episode
+    fn = lib.sch_episode_nodes_serial if nodes_serial else lib.sch_episode_nodes if nodes_kernel else lib.sch_episode_level if level else lib.sch_episode
     rc = fn(*args)
     return rc, obs, rew, stock, (tk, val, size)

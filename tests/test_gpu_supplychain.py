@@ -12,7 +12,18 @@ from oracle.supplychain import SupplyChainOracle
 pytestmark = pytest.mark.gpu
 CASES = sc_cases()
 DEV = "cuda"
-KERNELS = ["lane", "level", "staged"]
+KERNELS = ["lane", "level", "staged", "nodes"]
+
+
+def _or_skip(make, kernel):
+    """make(), skipping when the node-parallel kernel cannot take the chain (its block's
+    heaps and inbox must fit LDS; scg_sc_prepare rejects it otherwise)."""
+    try:
+        return make()
+    except ValueError as e:
+        if kernel == "nodes" and "node-parallel" in str(e):
+            pytest.skip(f"chain too wide for the node-parallel kernel: {e}")
+        raise
 
 
 def _vec(meta, n, **kw):
@@ -39,7 +50,7 @@ def test_step_matches_reference(name, kernel):
     g = load_sc(name)
     meta = g["meta"]
     T, N = meta["T"], g["obs"].shape[1]
-    env = _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, kernel=kernel)
+    env = _or_skip(lambda: _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, kernel=kernel), kernel)
     assert env.kernel == kernel
     dem, lts = env.draw_tables(0)
     assert np.array_equal(dem.cpu().numpy(), g["demands"])
@@ -62,6 +73,29 @@ def test_step_matches_reference(name, kernel):
     env.check_errors()
     with pytest.raises(IndexError):
         env.step(acts[0])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_nodes_kernel_serial_walk_matches_reference(name):
+    """The node-parallel kernel's path for envs whose receive order it cannot prove
+    (sc_nodes_serial: the nodes one after another on the staged heaps), forced for every
+    env with SCG_SC_SERIAL, against the reference's golden vectors."""
+    from gym_supplychain_amd import _native as nat
+    g = load_sc(name)
+    meta = g["meta"]
+    T, N = meta["T"], g["obs"].shape[1]
+    env = _or_skip(lambda: _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, kernel="nodes"), "nodes")
+    env._flags |= nat.SCG_SC_SERIAL
+    env.reset()
+    acts = torch.as_tensor(g["actions"], device=DEV)
+    for t in range(T):
+        obs, rew, _, _ = env.step(acts[t])
+        assert np.array_equal(obs.cpu().numpy(), g["obs"][t + 1]), (name, t)
+        assert np.array_equal(rew.cpu().numpy(), g["reward"][t]), (name, t)
+        assert np.array_equal(env.stock.cpu().numpy(), g["stock"][t + 1]), (name, t)
+    for n in range(N):
+        _check_heaps(env, g, T, n, name)
+    env.check_errors()
 
 
 @pytest.mark.parametrize("name", ["2perstage", "2perstage_stoch"])
@@ -119,8 +153,8 @@ def test_full_size_sampled_envs_match_oracle(scenario, n_envs, steps, kernel):
     import gym_supplychain_amd as gsa
     kw = {} if scenario == "sc-2perstage-v0" else dict(nodes_per_echelon=[8, 8, 8, 16])
     seed = 77
-    env = gsa.make_vec(scenario, n_envs, seed=seed, device=DEV, obs_dtype=torch.float64, auto_reset=False,
-                       kernel=kernel, **kw)
+    env = _or_skip(lambda: gsa.make_vec(scenario, n_envs, seed=seed, device=DEV, obs_dtype=torch.float64,
+                                        auto_reset=False, kernel=kernel, **kw), kernel)
     sp = env.spec
     nodes_info = (gsa.envs.scenarios.SCENARIOS[scenario](**kw))[0]
     okw = dict(num_products=sp.P, demand_range=sp.demand_range, processing_ratio=sp.processing_ratio,
@@ -216,8 +250,13 @@ def test_level_kernel_equals_lane_kernel(scenario, kw):
     widths (3, 5, 2, 7) and a tail block: identical obs, rewards, returns and stocks."""
     import gym_supplychain_amd as gsa
     N = 3001
-    envs = [gsa.make_vec(scenario, N, seed=21, device=DEV, obs_dtype=torch.float64, kernel=k, **kw) for k in KERNELS]
-    assert [e.kernel for e in envs] == KERNELS
+    envs = []
+    for k in KERNELS:
+        try:
+            envs.append(gsa.make_vec(scenario, N, seed=21, device=DEV, obs_dtype=torch.float64, kernel=k, **kw))
+        except ValueError as e:  # the node-parallel kernel only takes chains whose block fits LDS
+            assert k == "nodes" and "node-parallel" in str(e)
+    assert [e.kernel for e in envs] == KERNELS[:len(envs)]
     o = [e.reset() for e in envs]
     assert torch.equal(o[0], o[1])
     gen = torch.Generator(device=DEV).manual_seed(3)
@@ -351,6 +390,7 @@ def test_auto_kernel_symbols():
 # ---- full horizon at the BASELINE sizes (configs 3 and 4), into a second episode ---------
 FULL_CASES = {
     "2perstage": ("sc-2perstage-v0", 65536, {}),
+    "2perstage_nodes": ("sc-2perstage-v0", 65536, {"kernel": "nodes"}),
     "ntom": ("sc-Nperstage-multiproduct-v0", 262144, dict(nodes_per_echelon=[8, 8, 8, 16])),
     "ntom_stoch": ("sc-Nperstage-multiproduct-v0", 262144,
                    dict(nodes_per_echelon=[8, 8, 8, 16], stochastic_leadtimes=True, avg_leadtime=2, max_leadtime=4)),
@@ -370,8 +410,11 @@ def test_full_horizon_episode_matches_oracle(case):
     import gym_supplychain_amd as gsa
     from sc_replay import replay
     scenario, N, kw = FULL_CASES[case]
+    kw = dict(kw)
+    kernel = kw.pop("kernel", "auto")
     seed, extra = 1234, 3
-    env = gsa.make_vec(scenario, N, seed=seed, device=DEV, obs_dtype=torch.float64, auto_reset=True, **kw)
+    env = gsa.make_vec(scenario, N, seed=seed, device=DEV, obs_dtype=torch.float64, auto_reset=True, kernel=kernel,
+                       **kw)
     sp = env.spec
     T = sp.total_time_steps
     sample = sorted({0, 1, 63, 64, 65, 127, 4095, 4096, N // 3, N // 2, N // 2 + 1, N - 65, N - 64, N - 2, N - 1} |

@@ -130,6 +130,66 @@ def test_host_build_of_staged_kernel_matches_reference(harness, name):
         assert np.array_equal(led_v[:, 0], g["led_cost"][:, n]) and np.array_equal(led_k[:, 1], g["led_units_k"][:, n])
 
 
+@pytest.mark.parametrize("serial", [False, True])
+@pytest.mark.parametrize("name", CASES)
+def test_host_build_of_node_parallel_kernel_matches_reference(harness, name, serial):
+    """sc_step_nodes_kernel's phases (scg_supplychain_nodes.h) with the nodes run in REVERSE
+    order — every heap staged and its release summed without popping, every node acting on
+    that, every heap then replaying its pushes and pops — against the reference, exactly.
+    The inbox layout is the staged kernel's (the same scg_sc_prepare pass), so chains too
+    wide for the kernel's LDS are checked too. serial=True runs every step through the
+    kernel's fallback for unprovable receive orders (sc_nodes_serial) instead."""
+    import native_harness
+    from gym_supplychain_amd import _native as nat
+    g = load_sc(name)
+    meta = g["meta"]
+    spec, c, nodes, thr = _setup(g, nat.SC_KERNEL_STAGED)
+    P = spec.P
+    harness.sch_nodes_fallbacks()
+    for n in range(g["obs"].shape[1]):
+        rc, obs, rew, stock, (tk, val, size) = native_harness.run_episode(
+            harness, c, nodes, thr, meta["seed"], n, 0, g["actions"][:, n], nodes_kernel=True, nodes_serial=serial)
+        assert rc == 0
+        assert np.array_equal(obs, g["obs"][:, n]), name
+        assert np.array_equal(rew, g["reward"][:, n]), name
+        assert np.array_equal(stock.reshape(stock.shape[0], -1, P), g["stock"][:, n])
+        gt = g["heap_t"][:, n].reshape(len(obs), -1, g["heap_t"].shape[-1])
+        gv = g["heap_v"][:, n].reshape(gt.shape)
+        for s_ in range(len(obs)):
+            for hp in range(gt.shape[1]):
+                k = int(size[s_, hp])
+                assert (tk[s_, hp, :k] >> 3).tolist() == gt[s_, hp, :k].tolist()
+                assert val[s_, hp, :k].tolist() == gv[s_, hp, :k].tolist()
+    # the one-lane fallback is for amounts NumPy ties at float32 precision: none in these cases
+    assert harness.sch_nodes_fallbacks() == 0, name
+
+
+def test_recv_scan_flags_float32_ties():
+    """sc_recv_scan's fallback condition: two due amounts NumPy compares as equal (a float32
+    against a Python float, compared in float32) with different doubles make the heappop
+    order depend on the heap's shape, so the node-parallel kernel must not sum them itself."""
+    import ctypes
+    import native_harness
+    lib = native_harness.build()
+    f = lib.sch_recv_scan
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+
+    def scan(entries, t):
+        tk = np.array([(tt << 3) | k for tt, k, _ in entries], dtype=np.int32)
+        v = np.array([x for _, _, x in entries], dtype=np.float64)
+        out = ctypes.c_double()
+        ok = f(tk.ctypes.data, v.ctypes.data, len(entries), t, ctypes.byref(out))
+        return ok, out.value
+    F32, PYF, F64, INT = 3, 1, 7, 0
+    third32 = float(np.float32(1 / 3))
+    assert scan([(5, F32, 0.5), (5, F64, 0.25), (6, F32, 9.0)], 5) == (1, 0.25 + 0.5)
+    assert scan([(5, F32, third32), (5, PYF, 1 / 3)], 5)[0] == 0       # tied in float32, doubles differ
+    assert scan([(5, F64, third32), (5, PYF, 1 / 3)], 5)[0] == 1       # compared exactly: ordered
+    assert scan([(5, F32, 2.0), (5, INT, 2.0)], 5) == (1, 4.0)          # tied, same double
+    assert scan([(4, F32, 1.0), (5, F32, 2.0)], 5)[0] == 0              # overdue entry
+
+
 def test_auto_kernel_choice():
     """kernel='auto' (scg_sc_prepare, host only): the lane kernel with every heap in LDS when
     a block's heaps fit (2-per-stage), the node-staged kernel on the wide ntom chain."""

@@ -149,10 +149,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "staged", "all", "both"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "staged", "nodes", "all", "both"])
     a = ap.parse_args()
-    kernels = ["lane", "level", "staged"] if a.kernel in ("all", "both") else [a.kernel]
     for name in (["2perstage", "ntom"] if a.scenario == "both" else [a.scenario]):
+        kernels = [a.kernel]
+        if a.kernel in ("all", "both"):  # the node-parallel kernel only takes chains whose block fits LDS
+            kernels = ["lane", "level", "staged"] + (["nodes"] if name == "2perstage" else [])
         for k in kernels:
             run(name, a.steps, a.warmup, a.envs, not a.no_cpu_baseline and k == kernels[-1], k)
 
