@@ -679,9 +679,17 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   cfg->group = 1;
   cfg->inbox_size = 0;
   cfg->level_staged = 0;
-  // auto: the lane kernel with every heap in LDS when a block's heaps fit, else the
-  // node-staged kernel when the chain qualifies (measured faster than the lane kernel on
-  // HBM heaps), else the lane kernel on HBM heaps
+  // auto: the node-parallel kernel when every node gets a wave of its own and two blocks
+  // fit a CU's LDS (sc-2perstage-v0: 48 us against the LDS lane kernel's 68 us per step on
+  // MI355X); else the lane kernel with every heap in LDS when a block's heaps
+  // fit; else the node-staged kernel when the chain qualifies (measured faster than the lane
+  // kernel on HBM heaps); else the lane kernel on HBM heaps
+  if (want == SCG_SC_KERNEL_AUTO && NN <= sc_nodes_waves(NN) && maxd <= sc_nodes_max_dests() && H <= 64) {
+    std::vector<scg_sc_node> probe(nodes, nodes + NN);
+    const int entries = sc_inbox_layout(cfg, probe.data());
+    if (entries >= 0 && 2 * sc_nodes_lds_bytes(NN, P, H, entries, sc_nodes_waves(NN)) <= sc_nodes_lds_max())
+      want = SCG_SC_KERNEL_NODES;
+  }
   if (want == SCG_SC_KERNEL_AUTO && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
     std::vector<scg_sc_node> probe(nodes, nodes + NN);
     if (sc_inbox_layout(cfg, probe.data()) >= 0) want = SCG_SC_KERNEL_STAGED;

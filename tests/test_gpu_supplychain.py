@@ -373,13 +373,15 @@ def test_drop_in_env_build_info():
 
 
 def test_auto_kernel_symbols():
-    """kernel='auto' on the bench configs: the lane kernel with heaps in LDS (config 3), the
+    """kernel='auto' on the bench configs: the node-parallel kernel (config 3), the
     node-staged kernel (config 4); kernel_symbol names what rocprofv3 reports."""
     import gym_supplychain_amd as gsa
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV)
+    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2>"
+    env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, kernel="lane")
     assert env.kernel == "lane" and env.kernel_symbol == "scg::sc_step_lds_kernel<2, 32>"
     cus = torch.cuda.get_device_properties(DEV).multi_processor_count
-    env = gsa.make_vec("sc-2perstage-v0", cus * 512, device=DEV)
+    env = gsa.make_vec("sc-2perstage-v0", cus * 512, device=DEV, kernel="lane")
     assert env.kernel_symbol == "scg::sc_step_lds_kernel<2, 64>"
     env = gsa.make_vec("sc-Nperstage-multiproduct-v0", 64, device=DEV, nodes_per_echelon=[8, 8, 8, 16])
     assert env.kernel == "staged" and env.kernel_symbol == "scg::sc_step_staged_kernel<16>"
@@ -389,7 +391,7 @@ def test_auto_kernel_symbols():
 
 # ---- full horizon at the BASELINE sizes (configs 3 and 4), into a second episode ---------
 FULL_CASES = {
-    "2perstage": ("sc-2perstage-v0", 65536, {}),
+    "2perstage_lane": ("sc-2perstage-v0", 65536, {"kernel": "lane"}),
     "2perstage_nodes": ("sc-2perstage-v0", 65536, {"kernel": "nodes"}),
     "ntom": ("sc-Nperstage-multiproduct-v0", 262144, dict(nodes_per_echelon=[8, 8, 8, 16])),
     "ntom_stoch": ("sc-Nperstage-multiproduct-v0", 262144,
@@ -460,8 +462,10 @@ def test_lds_kernel_block_sizes_agree():
     import gym_supplychain_amd as gsa
     cus = torch.cuda.get_device_properties(DEV).multi_processor_count
     n_small, n_big = 1000, cus * 512 + 1000
-    small = gsa.make_vec("sc-2perstage-v0", n_small, seed=5, device=DEV, obs_dtype=torch.float64, auto_reset=True)
-    big = gsa.make_vec("sc-2perstage-v0", n_big, seed=5, device=DEV, obs_dtype=torch.float64, auto_reset=True)
+    small = gsa.make_vec("sc-2perstage-v0", n_small, seed=5, device=DEV, obs_dtype=torch.float64, auto_reset=True,
+                         kernel="lane")
+    big = gsa.make_vec("sc-2perstage-v0", n_big, seed=5, device=DEV, obs_dtype=torch.float64, auto_reset=True,
+                       kernel="lane")
     assert small.kernel_symbol.endswith(", 32>") and big.kernel_symbol.endswith(", 64>")
     o1, o2 = small.reset(), big.reset()
     assert torch.equal(o1, o2[:n_small])

@@ -33,6 +33,10 @@ def main():
     ap.add_argument("-D", dest="defines", action="append", default=[])
     ap.add_argument("--replace", nargs=3, action="append", default=[], metavar=("FILE", "OLD", "NEW"),
                     help="csrc/FILE: replace the exact text OLD by NEW (it must occur); for ablations")
+    ap.add_argument("--reuse-objs", action="store_true",
+                    help="reuse the tree's objects for sources whose text (and every header) is unchanged; "
+                         "for variants confined to one translation unit (-D flags are then assumed to only "
+                         "matter there)")
     a = ap.parse_args()
     root = os.path.join(REPO, "exp", a.name)
     shutil.rmtree(root, ignore_errors=True)
@@ -73,6 +77,16 @@ def main():
                         ignore=shutil.ignore_patterns("*.so", "__pycache__"))
     out = os.path.join(pkg, "libscgpu.so")
     srcs = [os.path.join(csrc, s) for s in build_native.SOURCES]
+    if a.reuse_objs:
+        tree_csrc, tree_objs = os.path.join(PKG, "csrc"), build_native.OUT + ".objs"
+        same = lambda f: open(os.path.join(csrc, f)).read() == open(os.path.join(tree_csrc, f)).read()  # noqa: E731
+        headers_same = all(same(f) for f in os.listdir(csrc) if f.endswith(".h")) and \
+            open(os.path.join(inc, "scgpu.h")).read() == open(os.path.join(REPO, "include", "scgpu.h")).read()
+        os.makedirs(out + ".objs", exist_ok=True)
+        for s_ in build_native.SOURCES:
+            obj = os.path.splitext(s_)[0] + ".o"
+            if headers_same and same(s_) and os.path.exists(os.path.join(tree_objs, obj)):
+                shutil.copyfile(os.path.join(tree_objs, obj), os.path.join(out + ".objs", obj))  # fresh mtime
     build_native.compile_library(out, srcs, [inc, csrc], extra=[f"-D{d}" for d in a.defines], verbose=False)
     import sysconfig
     bout = os.path.join(pkg, "_scgpu_fast" + sysconfig.get_config_var("EXT_SUFFIX"))
