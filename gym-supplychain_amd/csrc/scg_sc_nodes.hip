@@ -8,14 +8,15 @@
 // once, so the same work hides its latencies behind W times as many waves.
 //
 // LDS per block (doubles first): the block's heaps [NP][H][64], released sums [NP][64],
-// shipment inbox [E][64], node costs [NN][64]; then the int32 heap times/kinds, heap sizes,
-// inbox times/kinds, cost kinds and the per-wave "order not provable" flags [W][64].
-//   stage  (wave w, its nodes)  heaps HBM -> LDS, released sums, flags      | barrier
+// shipment inbox [E][64], node costs [NN][64], the stocks a step started from [NP][64]; then
+// the int32 heap times/kinds, heap sizes, inbox times/kinds, cost kinds and the per-wave
+// "order not provable" flags [W][64].
+//   stage  (wave w, its nodes)  heaps HBM -> LDS, released sums, flags
 //   act    (wave w, its nodes)  stock, costs, shipments -> inbox, stock obs | barrier
 //   heaps  (wave w, its nodes)  inbox pushes, pops, supply push, bins, copy back
 //   reward (wave 0)             -(costs in node order), return, demand / time obs, reset
-// An env any wave flagged skips act and heaps; wave 0 then steps it alone on its staged
-// heaps, node after node in the reference's order (sc_nodes_serial).
+// An env any wave flagged skips heaps; wave 0 puts its stocks back and steps it alone on its
+// staged heaps, node after node in the reference's order (sc_nodes_serial).
 #include <hip/hip_runtime.h>
 
 #include "scg_common.h"
@@ -45,27 +46,14 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   double* recv = hval + static_cast<int64_t>(NP) * H * 64;
   double* ibval = recv + NP * 64;
   double* cost_v = ibval + static_cast<int64_t>(E) * 64;
-  int32_t* htk = reinterpret_cast<int32_t*>(cost_v + NN * 64);
+  double* stock0 = cost_v + NN * 64;
+  int32_t* htk = reinterpret_cast<int32_t*>(stock0 + NP * 64);
   int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
   int32_t* ibtk = hsz + NP * 64;
   int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
   int32_t* amb = cost_k + NN * 64;
   ScEnv g = env_view(a, n, a.episode);
   auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
-
-  // stage
-  bool bad = false;
-  if (live)
-    for (int i = w; i < NN; i += W)
-      for (int p = 0; p < P; ++p) {
-        const int hp = i * P + p;
-        bad |= !sc_nodes_stage(c, g, lheap(hp), hsz[hp * 64 + lane], a.t, i, p, recv[hp * 64 + lane]);
-      }
-  amb[w * 64 + lane] = bad ? 1 : 0;
-  __syncthreads();
-  bool flagged = (a.flags & 4) != 0;
-  for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
-  const bool go = live && !flagged;
 
   // node observations go to obs, or to the terminal observation when the env resets now
   const bool terminal = a.flags & 1;
@@ -81,15 +69,27 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   const NodesInbox in{ibtk + lane, ibval + lane, 64};
   const float* act = a.act + n * c.A;
 
-  // act
-  if (go)
+  // stage, then act at once (no barrier between): a node's act needs only what its own heaps
+  // release. The stock it starts from is kept, so an env some wave flags is put back and
+  // stepped by the serial walk below.
+  bool bad = false;
+  if (live)
     for (int i = w; i < NN; i += W) {
+      for (int p = 0; p < P; ++p) {
+        const int hp = i * P + p;
+        stock0[hp * 64 + lane] = a.stock[hp * a.n + n];
+        bad |= !sc_nodes_stage(c, g, lheap(hp), hsz[hp * 64 + lane], a.t, i, p, recv[hp * 64 + lane]);
+      }
       const Num cst = sc_nodes_act<MAXD>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
       cost_v[i * 64 + lane] = cst.v;
       cost_k[i * 64 + lane] = cst.k;
       for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
     }
+  amb[w * 64 + lane] = bad ? 1 : 0;
   __syncthreads();
+  bool flagged = (a.flags & 4) != 0;
+  for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
+  const bool go = live && !flagged;
 
   // heaps
   if (go)
@@ -106,7 +106,8 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   // reward
   if (w == 0 && live) {
     double reward;
-    if (flagged) {  // every other wave left this env alone: its heaps are as staged
+    if (flagged) {  // its stocks back as they were; no wave touched its heaps: they are as staged
+      for (int hp = 0; hp < NP; ++hp) a.stock[hp * a.n + n] = stock0[hp * 64 + lane];
       reward = sc_nodes_serial<MAXD>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
     } else {
       Num total = pyint(0);
@@ -140,7 +141,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
 // LDS bytes of one block (the layout above).
 size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W) {
   const size_t NP = static_cast<size_t>(n_nodes) * P;
-  return 64 * ((NP * H + NP + E + n_nodes) * 8 + (NP * H + NP + E + n_nodes + W) * 4);
+  return 64 * ((NP * H + 2 * NP + E + n_nodes) * 8 + (NP * H + NP + E + n_nodes + W) * 4);
 }
 
 // Widest destination list the kernel is instantiated for (its split runs in registers).
