@@ -24,6 +24,25 @@
 #include "scg_supplychain_args.h"
 #include "scg_supplychain_nodes.h"
 
+// Diagnostic build only (-DSCG_NODES_STAMPS, tools/nodes_stamps.py): lane 0 of every wave
+// records the shader clock at the phase boundaries (0 start, 1 staged+acted, 2 past the
+// barrier, 3 heaps done, 4 end) into a buffer of its own that scg_nodes_debug_stamps copies
+// out; nothing else reads it. In the product build NSTAMP is empty.
+#ifdef SCG_NODES_STAMPS
+constexpr int kNStampSlots = 8;
+constexpr int kNStampWaves = 1 << 14;
+__device__ unsigned long long g_nodes_stamps[kNStampWaves * kNStampSlots];
+#define NSTAMP(k)                                                                                   \
+  do {                                                                                              \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                                   \
+    const unsigned w_ = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;                        \
+    if ((threadIdx.x & 63u) == 0 && w_ < static_cast<unsigned>(kNStampWaves))                       \
+      g_nodes_stamps[w_ * kNStampSlots + (k)] = now_;                                               \
+  } while (0)
+#else
+#define NSTAMP(k)
+#endif
+
 namespace scg {
 
 constexpr int kNodesMaxWaves = 8;
@@ -54,6 +73,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   int32_t* amb = cost_k + NN * 64;
   ScEnv g = env_view(a, n, a.episode);
   auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
+  NSTAMP(0);
 
   // node observations go to obs, or to the terminal observation when the env resets now
   const bool terminal = a.flags & 1;
@@ -86,7 +106,9 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
       for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
     }
   amb[w * 64 + lane] = bad ? 1 : 0;
+  NSTAMP(1);
   __syncthreads();
+  NSTAMP(2);
   bool flagged = (a.flags & 4) != 0;
   for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
   const bool go = live && !flagged;
@@ -101,6 +123,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
         sc_nodes_heap(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, a.t, i, p, a_i, lt_i, sink);
       }
     }
+  NSTAMP(3);
   if (autoreset) __syncthreads();  // the reset below rewrites heaps the other waves store
 
   // reward
@@ -136,6 +159,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
     }
   }
   if (live && g.overflow) atomicOr(a.err, 1);
+  NSTAMP(4);
 }
 
 // LDS bytes of one block (the layout above).
@@ -181,3 +205,15 @@ int sc_launch_nodes(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t 
 }
 
 }  // namespace scg
+
+#ifdef SCG_NODES_STAMPS
+// Diagnostic build only: copy the stamps of the first `waves` waves to host memory.
+extern "C" __attribute__((visibility("default"))) int scg_nodes_debug_stamps(unsigned long long* host, int waves) {
+  if (waves > kNStampWaves) waves = kNStampWaves;
+  if (hipDeviceSynchronize() != hipSuccess) return scg::fail(SCG_ERR_HIP, "sync");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nodes_stamps), sizeof(unsigned long long) * kNStampSlots * waves) !=
+      hipSuccess)
+    return scg::fail(SCG_ERR_HIP, "stamp copy");
+  return SCG_OK;
+}
+#endif

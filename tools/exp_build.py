@@ -34,9 +34,8 @@ def main():
     ap.add_argument("--replace", nargs=3, action="append", default=[], metavar=("FILE", "OLD", "NEW"),
                     help="csrc/FILE: replace the exact text OLD by NEW (it must occur); for ablations")
     ap.add_argument("--reuse-objs", action="store_true",
-                    help="reuse the tree's objects for sources whose text (and every header) is unchanged; "
-                         "for variants confined to one translation unit (-D flags are then assumed to only "
-                         "matter there)")
+                    help="reuse the tree's up-to-date objects for sources whose text (and every header) is "
+                         "unchanged and names none of the -D macros")
     a = ap.parse_args()
     root = os.path.join(REPO, "exp", a.name)
     shutil.rmtree(root, ignore_errors=True)
@@ -83,9 +82,13 @@ def main():
         headers_same = all(same(f) for f in os.listdir(csrc) if f.endswith(".h")) and \
             open(os.path.join(inc, "scgpu.h")).read() == open(os.path.join(REPO, "include", "scgpu.h")).read()
         os.makedirs(out + ".objs", exist_ok=True)
+        macros = [d.split("=")[0] for d in a.defines]
         for s_ in build_native.SOURCES:
             obj = os.path.splitext(s_)[0] + ".o"
-            if headers_same and same(s_) and os.path.exists(os.path.join(tree_objs, obj)):
+            tobj = os.path.join(tree_objs, obj)
+            text = open(os.path.join(csrc, s_)).read()
+            fresh = os.path.exists(tobj) and os.path.getmtime(tobj) >= os.path.getmtime(os.path.join(tree_csrc, s_))
+            if headers_same and same(s_) and fresh and not any(m in text for m in macros):
                 shutil.copyfile(os.path.join(tree_objs, obj), os.path.join(out + ".objs", obj))  # fresh mtime
     build_native.compile_library(out, srcs, [inc, csrc], extra=[f"-D{d}" for d in a.defines], verbose=False)
     import sysconfig

@@ -1,0 +1,67 @@
+"""Where a node-parallel SupplyChain kernel wave spends its time (diagnostic build only).
+
+    python tools/exp_build.py nstamps --reuse-objs -D SCG_NODES_STAMPS
+    SCG_PKG_ROOT=exp/nstamps python tools/nodes_stamps.py [--envs 65536] [--steps 3]
+
+Runs sc-2perstage-v0 steps with kernel="nodes"; after each, reads the shader-clock stamps
+lane 0 of every wave wrote (scg_sc_nodes.hip NSTAMP: 0 start, 1 staged+acted, 2 past the
+barrier, 3 heaps done, 4 end) and prints per phase the median / p90 over waves, split by
+wave index in the block (wave w runs node w), and the spread of wave starts and ends
+(shader clocks, relative to the earliest start).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.environ.get("SCG_PKG_ROOT") or os.path.join(REPO, "gym-supplychain_amd"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import gym_supplychain_amd as gsa
+    from gym_supplychain_amd import _native as nat
+    fn = nat.lib.scg_nodes_debug_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    env = gsa.make_vec("sc-2perstage-v0", a.envs, seed=0, device=dev, obs_dtype=torch.float32, auto_reset=True,
+                       kernel="nodes")
+    W = env._cfg.group
+    waves = (a.envs + 63) // 64 * W
+    env.reset()
+    gen = torch.Generator(device=dev).manual_seed(0)
+    for _ in range(10):
+        env.step(torch.rand((a.envs, env.n_actions), generator=gen, device=dev) * 2 - 1)
+    buf = np.zeros((min(waves, 1 << 14), 8), dtype=np.uint64)
+    for s in range(a.steps):
+        act = torch.rand((a.envs, env.n_actions), generator=gen, device=dev) * 2 - 1
+        torch.cuda.synchronize()
+        env.step(act)
+        torch.cuda.synchronize()
+        assert fn(buf.ctypes.data, buf.shape[0]) == 0
+        st = buf.astype(np.int64)
+        t0 = st[:, 0].min()
+        rel = st[:, :5] - t0
+        out = {"step": s, "waves": int(len(st)), "span": int(rel[:, 4].max()),
+               "start_p50_p90_max": [int(np.percentile(rel[:, 0], q)) for q in (50, 90, 100)],
+               "end_p10_p50_max": [int(np.percentile(rel[:, 4], q)) for q in (10, 50, 100)]}
+        names = ["stage+act", "barrier", "heaps", "reward/end", "whole"]
+        d = np.stack([rel[:, 1] - rel[:, 0], rel[:, 2] - rel[:, 1], rel[:, 3] - rel[:, 2], rel[:, 4] - rel[:, 3],
+                      rel[:, 4] - rel[:, 0]], 1)
+        out["phase_p50_p90"] = {n: [int(np.percentile(d[:, k], 50)), int(np.percentile(d[:, k], 90))]
+                                for k, n in enumerate(names)}
+        wi = np.arange(len(st)) % W
+        out["by_wave_p50"] = {n: [int(np.median(d[wi == w, k])) for w in range(W)] for k, n in enumerate(names)}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
