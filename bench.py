@@ -18,11 +18,12 @@ Timing (rank 0 prints ONE JSON line):
     both. The collector is off from there on;
   * the timed region is exactly K steps, bracketed by barrier + synchronize, max over
     ranks; `value` = envs of all ranks x K / that wall time. Nothing inside is stamped
-    except the first and the last launch, whose own dispatch begin / end timestamps
-    (hipExtLaunchKernel) give the region's GPU time: `roofline.avg_kernel_us` = that / K;
-  * `episodes_timed`: the same measurement over 100 whole episodes (3,500 steps), as
-    SURVEY §8(d) asks, reported beside the K-step headline;
-  * `roofline`: algorithmic bytes of the timed launches (DESIGN.md §6, 260 B per env on a
+    (stamping the first and last launch cost a K = 20 region 0.3-0.6 us per step,
+    profiles/r02s_stamped_headline_ab.log);
+  * `episodes_timed`: the same over 100 whole episodes (3,500 steps), as SURVEY §8(d)
+    asks, with its first and last launch stamped (hipExtLaunchKernel dispatch begin / end):
+    that GPU time / 3,500 is `roofline.avg_kernel_us`;
+  * `roofline`: algorithmic bytes of those 3,500 launches (DESIGN.md §6, 260 B per env on a
     regular week, summed week by week) / their GPU time, against the 8 TB/s spec and the
     peak a STREAM copy measures in the same run (`measured_peak`, `frac_measured_peak`);
     `traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary of this
@@ -338,8 +339,7 @@ def main():
     import gc
     gc.disable()  # no collector pass inside a timed region
     # headline: exactly K steps
-    timed_bytes = bytes_of(args.steps)
-    elapsed, gpu_ms = region(loop, args.steps, world, barrier, sync, (ev[0], ev[1], nat.hip_event_elapsed_ms))
+    elapsed, _ = region(loop, args.steps, world, barrier, sync)  # unstamped (profiles/r02s_stamped_headline_ab.log)
     gather.result()
     # 100 whole episodes, from an episode boundary
     loop.run((WEEKS - env.week) % WEEKS)
@@ -356,23 +356,22 @@ def main():
     for e in ev + [x for pair in iso for x in pair]:
         nat.hip_event_destroy(e)
     env.check_errors()
-    elapsed, gpu_ms, ep_elapsed, ep_gpu_ms, iso_ms = max_over_ranks([elapsed, gpu_ms, ep_elapsed, ep_gpu_ms, iso_ms],
-                                                                     world, device)
+    elapsed, ep_elapsed, ep_gpu_ms, iso_ms = max_over_ranks([elapsed, ep_elapsed, ep_gpu_ms, iso_ms], world, device)
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras:
         extras["measured_peak"] = stream_copy_peak(device)
         extras["beyond_cache"] = beyond_cache_point(device)
 
     if rank == 0:
-        achieved = timed_bytes / (gpu_ms / 1e3) / 1e9
+        achieved = ep_bytes / (ep_gpu_ms / 1e3) / 1e9
         traffic, traffic_src = pmc_traffic(n_envs=N)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": f"scg::{KERNEL} (L = 4, Poisson demand, state slab)",
-                "avg_kernel_us": gpu_ms * 1e3 / args.steps,
-                "avg_kernel_source": "first launch's dispatch begin to last launch's end (hipExtLaunchKernel stamps) "
-                                     "over the timed region",
-                "bytes_per_launch": timed_bytes / args.steps, "launches_timed": args.steps,
+                "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
+                "avg_kernel_source": "the 100-episode timed region: first launch's dispatch begin to last launch's "
+                                     "end (hipExtLaunchKernel stamps, nothing stamped in between) / launches",
+                "bytes_per_launch": ep_bytes / k_ep, "launches_timed": k_ep,
                 "isolated_kernel_us": iso_ms * 1e3 / k_samples, "isolated_launches": k_samples,
                 "isolated_frac": sampled_bytes / (iso_ms / 1e3) / 1e9 / HBM_PEAK_GBS}
         if "measured_peak" in extras:
