@@ -163,6 +163,17 @@ class StepLoop:
 
     def run(self, k, first=None, last=None, each=None, sync_each=None):
         env, acts = self.env, self.week_actions
+        if first is None and last is None and each is None and sync_each is None:
+            step, gather, T = env.step, self.gather, len(acts)
+            w = env.week
+            for _ in range(k):  # the timed path: one action row and one step call per week
+                info = step(acts[w])[3]
+                w = w + 1 if w + 1 < T else 0
+                if info:
+                    self.episodes += 1
+                    if gather is not None:
+                        gather.on_episode_end(info["episode_return"])
+            return
         for i in range(k):
             stamp = each[i] if each is not None else ((first, None) if i == 0 and first else None)
             if i == k - 1 and last is not None:
