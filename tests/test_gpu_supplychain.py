@@ -393,6 +393,8 @@ def test_auto_kernel_symbols():
 FULL_CASES = {
     "2perstage_lane": ("sc-2perstage-v0", 65536, {"kernel": "lane"}),
     "2perstage_nodes": ("sc-2perstage-v0", 65536, {"kernel": "nodes"}),
+    "2perstage_stoch_nodes": ("sc-2perstage-v0", 65536, {"kernel": "nodes", "stochastic_leadtimes": True,
+                                                          "avg_leadtime": 2, "max_leadtime": 4}),
     "ntom": ("sc-Nperstage-multiproduct-v0", 262144, dict(nodes_per_echelon=[8, 8, 8, 16])),
     "ntom_stoch": ("sc-Nperstage-multiproduct-v0", 262144,
                    dict(nodes_per_echelon=[8, 8, 8, 16], stochastic_leadtimes=True, avg_leadtime=2, max_leadtime=4)),
