@@ -181,13 +181,15 @@ size_t sc_nodes_lds_max() { return kNodesLdsMax; }
 
 template <int MAXD>
 int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
-  static bool raised = false;
+  static bool raised[64] = {};  // per device; setting it twice from racing threads is harmless
   const size_t lds = sc_nodes_lds_bytes(a.c.n_nodes, a.c.P, a.c.H, E, W);
-  if (lds > 64 * 1024 && !raised) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (lds > 64 * 1024 && !raised[dev]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sc_step_nodes_kernel<MAXD>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNodesLdsMax)) != hipSuccess)
       return fail(SCG_ERR_HIP, "node-parallel kernel: cannot raise its LDS limit");
-    raised = true;
+    raised[dev] = true;
   }
   hipLaunchKernelGGL(sc_step_nodes_kernel<MAXD>, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64 * W), lds, s,
                      a, W, E);
