@@ -27,6 +27,27 @@ def shard_offset(n_per_rank, rank=None):
     return int(rank) * int(n_per_rank)
 
 
+def _async_copy(dst, src):
+    """dst <- src, async on the current stream. On the GPU one hipMemcpyAsync (device to
+    device) through torch's HIP runtime: a torch copy_ costs the host ≈10 µs of dispatch,
+    a quarter of a 35-week episode's step budget at 65,536 envs."""
+    if dst.device.type != "cuda" or not (dst.is_contiguous() and src.is_contiguous()) or dst.dtype != src.dtype \
+            or dst.numel() != src.numel() or src.device != dst.device:
+        dst.copy_(src, non_blocking=True)
+        return
+    import ctypes
+
+    from . import _native as nat
+    hip = nat.hip_runtime()
+    if not getattr(hip, "_scg_memcpy_async", False):
+        hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        hip._scg_memcpy_async = True
+    rc = hip.hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), 3,  # D2D
+                            ctypes.c_void_p(nat.raw_stream(dst.device.index)))
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+
 class EpisodeReturnGather:
     """All-gather of every env's finished-episode return, overlapped with compute.
 
@@ -48,12 +69,12 @@ class EpisodeReturnGather:
 
     def on_episode_end(self, final_return):
         if self.world == 1:  # the snapshot is the result: one device copy per episode
-            self._out.copy_(final_return, non_blocking=True)
+            _async_copy(self._out, final_return)
             self.gathers += 1
             return
         if self._work is not None:
             self._work.wait()  # previous gather still reading _stage
-        self._stage.copy_(final_return, non_blocking=True)
+        _async_copy(self._stage, final_return)
         self._work = dist.all_gather_into_tensor(self._out, self._stage, group=self.group, async_op=True)
         self.gathers += 1
 

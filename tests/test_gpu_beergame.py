@@ -438,3 +438,30 @@ def test_overflow_reported_at_next_terminal_step_and_by_other_kernels():
     v2.step(zero)
     with pytest.raises(OverflowError):
         v2.check_errors()
+
+
+def test_episode_return_gather_snapshot_on_device():
+    """EpisodeReturnGather with one process: the per-env returns of a finished episode are
+    snapshotted on the launch stream (a device-to-device hipMemcpyAsync) and survive the next
+    episode overwriting the env's own buffer."""
+    from gym_supplychain_amd import BeerGameVecEnv
+    from gym_supplychain_amd.distributed import EpisodeReturnGather
+    N, T = 4096, 35
+    env = BeerGameVecEnv(N, {}, demand="poisson", poisson_lambda=8.0, seed=3, device=DEV, auto_reset=True,
+                         track_returns=True)
+    gather = EpisodeReturnGather(N, DEV)
+    env.reset()
+    acts = torch.randint(0, 9, (T, N, 4), dtype=torch.int32, device=DEV)
+    finals = []
+    for ep in range(2):
+        for w in range(T):
+            _, _, _, info = env.step(acts[w])
+            if info:
+                gather.on_episode_end(info["episode_return"])
+                finals.append(info["episode_return"].clone())
+                if ep == 0:
+                    snap = gather.result()
+                    first = snap.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(first, finals[0].to(torch.int64))
+    assert torch.equal(gather.result(), finals[1].to(torch.int64)) and gather.gathers == 2
