@@ -25,8 +25,8 @@
 #include "scg_supplychain_nodes.h"
 
 // Diagnostic build only (-DSCG_NODES_STAMPS, tools/nodes_stamps.py): lane 0 of every wave
-// records the shader clock at the phase boundaries (0 start, 1 staged+acted, 2 past the
-// barrier, 3 heaps done, 4 end) into a buffer of its own that scg_nodes_debug_stamps copies
+// records the shader clock at the phase boundaries (0 start, 5 heaps staged, 1 acted, 2 past
+// the barrier, 3 heaps done, 4 end) into a buffer of its own that scg_nodes_debug_stamps copies
 // out; nothing else reads it. In the product build NSTAMP is empty.
 #ifdef SCG_NODES_STAMPS
 constexpr int kNStampSlots = 8;
@@ -100,6 +100,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
         stock0[hp * 64 + lane] = a.stock[hp * a.n + n];
         bad |= !sc_nodes_stage(c, g, lheap(hp), hsz[hp * 64 + lane], a.t, i, p, recv[hp * 64 + lane]);
       }
+      NSTAMP(5);  // (the last node of the wave's) heaps staged, act next
       const Num cst = sc_nodes_act<MAXD>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
       cost_v[i * 64 + lane] = cst.v;
       cost_k[i * 64 + lane] = cst.k;
