@@ -78,21 +78,19 @@ def cpu_baseline(name, budget=1.5, max_procs=16):
 
 
 def pmc_traffic(symbol, n_envs, name):
-    """HBM bytes per launch of `symbol` from the latest committed PMC summary
-    (profiles/rNN_pmc_summary.json: tools/gpu_pmc.sh runs this tool at the default sizes with
-    the auto kernel; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM). None when absent or
+    """HBM bytes per launch of `symbol` from the newest committed PMC summary that has it
+    (profiles/r*_pmc_summary.json, e.g. tools/gpu_sc_traffic.sh at the default sizes with
+    the auto kernels; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM). None when absent or
     for another batch size."""
     import glob
     if n_envs != SCENARIOS[name]["n_envs"]:
         return None, None
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        traffic = json.load(f).get("traffic", {})
-    for k, t in traffic.items():
-        if symbol.split("::")[-1] in k and t.get("hbm_bytes_per_launch"):
-            return t["hbm_bytes_per_launch"], os.path.relpath(files[-1], REPO)
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
+        with open(path) as f:
+            traffic = json.load(f).get("traffic", {})
+        for k, t in traffic.items():
+            if symbol.split("::")[-1] in k and t.get("hbm_bytes_per_launch"):
+                return t["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
     return None, None
 
 
