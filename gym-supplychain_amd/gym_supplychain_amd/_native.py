@@ -278,6 +278,11 @@ def raw_stream(device_index):
     return torch.cuda.current_stream(device_index).cuda_stream
 
 
+def raw_stream_fn():
+    """raw_stream itself, or torch's C entry point when present (no Python frame per call)."""
+    return _raw_stream if _raw_stream is not None else raw_stream
+
+
 _hip = None
 
 

@@ -274,6 +274,7 @@ class BeerGameVecEnv:
         self._term_ptr = self._term_obs.data_ptr()
         self._cfg_addr, self._st_addr = ctypes.addressof(self._cfg), ctypes.addressof(self._st)
         self._fast_step, self._fast_step_timed = nat.fast.bg_step, nat.fast.bg_step_timed
+        self._raw_stream = nat.raw_stream_fn()  # torch's current raw stream, one C call
         self._ready = {}  # id(actions) -> (weakref, data_ptr) of validated action tensors
         # gym surface (an extension: the reference leaves both spaces unset, :62-64)
         self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
@@ -331,7 +332,7 @@ class BeerGameVecEnv:
             ptr = actions.data_ptr()
         if _events is None:
             r = self._fast_step(self._cfg_addr, self._st_addr, ptr, self._obs_ptr, self._rew_ptr,
-                                self._term_ptr, self._flags, nat.raw_stream(self._dev_index))
+                                self._term_ptr, self._flags, self._raw_stream(self._dev_index))
         else:  # (start, stop) hipEvent_t handles stamped with the kernel's own dispatch times
             r = self._fast_step_timed(self._cfg_addr, self._st_addr, ptr, self._obs_ptr,
                                       self._rew_ptr, self._term_ptr, self._flags, _events[0], _events[1],
