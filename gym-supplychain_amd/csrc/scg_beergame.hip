@@ -156,6 +156,13 @@ int check_state(const scg_bg_config* cfg, const scg_bg_state* st) {
   return SCG_OK;
 }
 
+// Weeks 1..init_slots hold the initial pipeline (beergame_env.py:52); the ring keeps those
+// within the horizon, a full table all of them.
+inline int32_t init_slots(const scg_bg_config* cfg) {
+  const int32_t d0 = cfg->shipment_delays ? cfg->shipment_delays[0] : 0;
+  return cfg->full_table ? d0 : std::min(d0, cfg->max_weeks);
+}
+
 BgArgs make_args(const scg_bg_config* cfg, const scg_bg_state* st) {
   BgArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -181,7 +188,7 @@ BgArgs make_args(const scg_bg_config* cfg, const scg_bg_state* st) {
   a.b = cfg->backlog_cost;
   a.ship_value = cfg->initial_shipment_value;
   a.orders_value = cfg->initial_orders_value;
-  a.init_slots = std::min(cfg->shipment_delays ? cfg->shipment_delays[0] : 0, cfg->max_weeks);
+  a.init_slots = init_slots(cfg);
   a.ring_slots = cfg->ring_slots;
   for (int l = 0; l < cfg->levels; ++l) a.init_inv[l] = cfg->initial_inventory[l];
   a.demand_lo = cfg->demand_lo;
@@ -263,17 +270,25 @@ int scg_bg_prepare(scg_bg_config* cfg) {
       return fail(SCG_ERR_INVALID, "stochastic delays need 0 <= delay_lo < delay_hi <= %d", SCG_BG_MAX_DELAY + 1);
     R = std::max(R, cfg->delay_hi);
   }
+  const bool full = cfg->full_table != 0;
+  if (full) {  // the reference's table: rows max(T+1, max_w(w+d_w+1)) + 1 (:46-50), slot s = week s
+    if (cfg->variant != 1) return fail(SCG_ERR_INVALID, "full_table is a BeerGameEnv (variant 1) option");
+    int32_t last = T + 1;
+    for (int32_t w = 0; w <= T; ++w) last = std::max(last, w + cfg->shipment_delays[w] + 1);
+    R = last + 1;
+    if (R > 127) return fail(SCG_ERR_INVALID, "full_table needs at most 127 rows (this config has %d)", R);
+  }
   // Which arrival weeks have been written, in week order (writes only target later weeks).
-  std::vector<uint8_t> written(static_cast<size_t>(T) + 2, 0);
-  const int32_t d0 = cfg->shipment_delays[0];
-  for (int32_t t = 1; t <= std::min(d0, T); ++t) written[t] = 1;  // initial pipeline (:52)
+  // (a full table also keeps the rows past T: week T + 1 + max delay at most)
+  std::vector<uint8_t> written(static_cast<size_t>(T) + SCG_BG_MAX_DELAY + 2, 0);
+  for (int32_t t = 1; t <= init_slots(cfg); ++t) written[t] = 1;  // initial pipeline (:52)
   cfg->plan[0] = 0;
   for (int32_t w = 1; w <= T; ++w) {
     const int32_t d = cfg->shipment_delays[w];
     int32_t mode;
     if (d == 0) {
       mode = MODE_DIRECT;                 // :93-94, :111-112
-    } else if (w + d > T) {
+    } else if (w + d > T && !full) {
       mode = MODE_DROP;                   // lands after the last step: never received
     } else if (written[w + d]) {
       mode = MODE_ADD;                    // several weeks ship into one arrival week
@@ -354,7 +369,7 @@ int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t*
     sa.demand_hi = cfg->demand_hi;
     sa.ship_value = cfg->initial_shipment_value;
     sa.orders_value = cfg->initial_orders_value;
-    sa.init_slots = std::min(cfg->shipment_delays ? cfg->shipment_delays[0] : 0, cfg->max_weeks);
+    sa.init_slots = init_slots(cfg);
     sa.env_offset = st->env_offset;
     sa.guard = week_guard(cfg->levels, cfg->inv_cost, cfg->backlog_cost);
     sa.err_host = st->error_host;

@@ -256,6 +256,12 @@ __global__ __launch_bounds__(kBlock) void bg_reset_kernel(const BgArgs a) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (n >= a.n) return;
   reset_env<L>(a, n, a.obs);
+  // reset() starts clean: the int32-overflow word (and its host-mapped copy) is scoped to
+  // the episodes since the last reset, in stream order after every earlier launch
+  if (n == 0) {
+    if (a.err) *reinterpret_cast<volatile int32_t*>(a.err) = 0;
+    if (a.err_host) *reinterpret_cast<volatile int32_t*>(a.err_host) = 0;
+  }
 }
 
 // One week of one env (beergame_env.py:66-138), pure register arithmetic. The caller

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (loads the HIP runtime libscgpu.so binds to)
 
 LIB_NAME = "libscgpu.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 SCG_OK = 0
 SCG_ERR_INVALID = 1
@@ -73,6 +73,7 @@ class BgConfig(ctypes.Structure):
         ("stochastic_delays", ctypes.c_int32),
         ("delay_lo", ctypes.c_int32),
         ("delay_hi", ctypes.c_int32),
+        ("full_table", ctypes.c_int32),
     ]
 
 
@@ -308,7 +309,9 @@ class MappedWord:
         hip.hipHostFree.argtypes = [ctypes.c_void_p]
         hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
         host = ctypes.c_void_p()
-        if hip.hipHostMalloc(ctypes.byref(host), 64, 0x2) != 0:  # hipHostMallocMapped
+        # hipHostMallocMapped | hipHostMallocCoherent: the kernel's store reaches the host
+        # without depending on HIP_HOST_COHERENT
+        if hip.hipHostMalloc(ctypes.byref(host), 64, 0x2 | 0x40000000) != 0:
             raise RuntimeError("hipHostMalloc failed")
         dev = ctypes.c_void_p()
         if hip.hipHostGetDevicePointer(ctypes.byref(dev), host, 0) != 0:

@@ -39,10 +39,17 @@ ACTION_BOUND = 2 ** 15
 
 
 def _entropy_seed(seed):
-    """A Philox key: `seed`, or fresh OS entropy for None (RandomState(None) semantics)."""
-    if seed is None:
-        return int.from_bytes(os.urandom(8), "little")
-    return int(seed) & 0xFFFFFFFFFFFFFFFF
+    """A Philox key: `seed`, or fresh OS entropy for None (RandomState(None) semantics).
+
+    Under torch.distributed the entropy is rank 0's, broadcast to every rank, so shards
+    of one seed=None batch keep drawing the demand one big batch would (env_offset)."""
+    if seed is not None:
+        return int(seed) & 0xFFFFFFFFFFFFFFFF
+    key = [int.from_bytes(os.urandom(8), "little")]
+    dist = torch.distributed
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast_object_list(key, src=0)
+    return key[0]
 
 
 def _int32(name, v):
@@ -121,6 +128,8 @@ class BeerGameVecEnv:
     state_slab: hold the state in one slab (scg_bg_slab_layout) so step() runs the slab
             kernel (default; needs N * L % 4 == 0, else separate buffers and the general
             kernel). Both give identical results.
+    full_table: keep the reference's whole absolute-week shipment table (beergame_env.py:46-50)
+            instead of the ring of max delay + 1 weeks (`shipment_table()`); at most 127 rows.
     Values the reference keeps in int64 are int32 here; a step whose int64 result leaves
     int32 sets a sticky device flag, raised as OverflowError by check_errors() and, one
     episode late (so the step loop never stalls), by the terminal step.
@@ -128,7 +137,7 @@ class BeerGameVecEnv:
 
     def __init__(self, n_envs, env_init_info=None, demand="fixed", poisson_lambda=8.0, seed=0, device=None,
                  env_offset=0, auto_reset=True, track_costs=True, track_history=False, track_returns=True,
-                 horizon=None, config=None, variant_fields=None, state_slab=True):
+                 horizon=None, config=None, variant_fields=None, state_slab=True, full_table=False):
         n_envs = int(n_envs)
         if n_envs < 1:
             raise ValueError("n_envs must be >= 1")
@@ -178,6 +187,7 @@ class BeerGameVecEnv:
             c.initial_inventory[i] = v
         c.demand_mode = mode
         c.demand_lo, c.demand_hi = demand_range
+        c.full_table = int(bool(full_table))
         for k, v in (variant_fields or {}).items():
             setattr(c, k, v)
         c.shipment_delays = ctypes.cast(self._delays, ctypes.c_void_p)
@@ -275,7 +285,7 @@ class BeerGameVecEnv:
         self._cfg_addr, self._st_addr = ctypes.addressof(self._cfg), ctypes.addressof(self._st)
         self._fast_step, self._fast_step_timed = nat.fast.bg_step, nat.fast.bg_step_timed
         self._raw_stream = nat.raw_stream_fn()  # torch's current raw stream, one C call
-        self._ready = {}  # id(actions) -> (weakref, data_ptr) of validated action tensors
+        self._ready = {}  # id(actions) -> (weakref, data_ptr, stride) of validated action tensors
         # gym surface (an extension: the reference leaves both spaces unset, :62-64)
         self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
         # actions: the reference's are unbounded int64 (:121); sampled ones stay within
@@ -290,6 +300,8 @@ class BeerGameVecEnv:
         return nat.raw_stream(self._dev_index)
 
     def reset(self):
+        """Reset every env; the reset kernel also clears the int32-overflow word (and its
+        host-mapped copy), so an overflow is scoped to the episodes since the last reset()."""
         nat.check(nat.lib.scg_bg_reset(self._cfg_ref, self._st_ref, self._obs.data_ptr(), self._stream()))
         return self._obs
 
@@ -319,14 +331,16 @@ class BeerGameVecEnv:
     def step(self, actions, _events=None):
         # a tensor validated once is recognised by identity and data pointer (the policy's
         # per-week action buffers are reused), skipping the per-call checks
+        # (the stride catches in-place metadata changes that keep the pointer: t_(),
+        # as_strided_(), a shrinking resize_())
         ok = self._ready.get(id(actions))
-        if ok is not None and ok[0]() is actions and ok[1] == actions.data_ptr():
+        if ok is not None and ok[0]() is actions and ok[1] == actions.data_ptr() and ok[2] == actions.stride():
             ptr = ok[1]
         else:
             if self._is_ready(actions):
                 if len(self._ready) >= 64:
                     self._ready.clear()
-                self._ready[id(actions)] = (weakref.ref(actions), actions.data_ptr())
+                self._ready[id(actions)] = (weakref.ref(actions), actions.data_ptr(), actions.stride())
             else:
                 actions = self._actions(actions)
             ptr = actions.data_ptr()
@@ -446,6 +460,33 @@ class BeerGameVecEnv:
     def final_return(self):
         return self._final_ret
 
+    @property
+    def full_table(self):
+        return bool(self._cfg.full_table)
+
+    def scheduled_rows(self, week=None):
+        """Bool [R]: the shipment-table rows the current episode has scheduled by `week`
+        (default: now) — weeks 1..d0 of the initial pipeline (:52) and w + d_w for every
+        week w <= `week` with d_w > 0 (:96, :114). Host arithmetic on the config only."""
+        w = self.week if week is None else int(week)
+        R, d = self.ring_slots, self.config.shipment_delays
+        rows = np.zeros(R, dtype=bool)
+        rows[1: 1 + int(d[0])] = True
+        for k in range(1, max(w, 0) + 1):
+            if d[k] > 0 and k + d[k] < R:
+                rows[k + d[k]] = True
+        return rows
+
+    def shipment_table(self):
+        """int64 [N, R, L]: the reference's absolute-week `shipments` table of every env
+        (beergame_env.py:46-52, :96, :114) — needs full_table=True. Row s is week s; rows
+        the episode has not scheduled yet read 0, as in the reference."""
+        if not self._cfg.full_table:
+            raise ValueError("shipment_table() needs BeerGameVecEnv(..., full_table=True)")
+        t = self._ring.permute(1, 0, 2).to(torch.int64)
+        mask = torch.as_tensor(self.scheduled_rows(), device=t.device)
+        return t * mask.view(1, -1, 1)
+
     def close(self):
         pass
 
@@ -457,12 +498,19 @@ class BeerGameEnv(spaces.Env):
     and step() give int64 observations, step() an np.int64 reward, a bool done and {}
     (:138). Stepping past the last week raises IndexError (:79 on customer_demand[T]).
     The week runs on the GPU as a batch of one; use BeerGameVecEnv for throughput.
+    State attributes (inventory, backlog, orders_placed, incoming_orders, shipments, the
+    ledgers, all_orders_placed) are read back from the device when accessed.
     """
 
     def __init__(self, env_init_info={}, device=None):  # noqa: B006 - reference signature (:11)
         self.DEBUG = False
+        cfg = BeerGameConfig(env_init_info)
+        # the reference's whole shipment table (:46-50) when it fits the kernels' 127 rows
+        d = cfg.shipment_delays.astype(np.int64)
+        rows = max(cfg.max_weeks + 1, int((np.arange(d.size) + d + 1).max())) + 1
         self._vec = BeerGameVecEnv(1, env_init_info, demand="fixed", device=device, auto_reset=False,
-                                   track_costs=True, track_history=True, track_returns=False)
+                                   track_costs=True, track_history=True, track_returns=False, config=cfg,
+                                   full_table=rows <= 127)
         cfg = self._vec.config
         self.levels = cfg.levels
         self.inv_cost = cfg.inv_cost
@@ -482,11 +530,13 @@ class BeerGameEnv(spaces.Env):
         self._out_np = self._out_host.numpy()
         self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
         self._err_np = self._err_host.numpy()
+        self._last_act = None
         self.week = None
 
     def reset(self):
         obs = self._vec.reset()
         self.week = 0
+        self._last_act = None
         self.current_state = obs[0].cpu().numpy().astype(np.int64)
         return self.current_state
 
@@ -506,6 +556,7 @@ class BeerGameEnv(spaces.Env):
             raise OverflowError("a BeerGame value left int32 range; the GPU state no longer matches the reference")
         L = self.levels
         self.week = self._vec.week
+        self._last_act = self._act_np[0].astype(np.int64)
         self.current_state = self._out_np[:L].astype(np.int64)
         reward = np.int64(self._out_np[L])
         if self.DEBUG:
@@ -540,14 +591,38 @@ class BeerGameEnv(spaces.Env):
     def all_orders_placed(self):
         return self._vec.all_orders_placed[0].cpu().numpy().astype(np.int64)
 
-    def render(self, mode='human'):  # beergame_env.py:158-175 (the pipeline rows are not kept)
+    @property
+    def incoming_orders(self):
+        """The order slips of the last week (:79-81): customer demand at level 0, the orders
+        of the level below above it — the kernel's orders_placed minus the action it added
+        (:121); the initial orders after reset() (:145)."""
+        if self._last_act is None:
+            return np.full(self.levels, self.initial_orders_value, dtype=np.int64)
+        return self.orders_placed - self._last_act
+
+    @property
+    def shipments(self):
+        """The reference's absolute-week table [rows, L] (:46-52): row w is what arrives in
+        week w, past weeks included (the table is never shifted, :73-74)."""
+        if not self._vec.full_table:
+            raise NotImplementedError("this horizon's shipment table has more than the kernels' 127 rows")
+        return self._vec.shipment_table()[0].cpu().numpy()
+
+    def render(self, mode='human'):  # beergame_env.py:158-175
         inv, bk = self.inventory, self.backlog
         print('\n' + '=' * 20)
         print('Week:\t', self.week)
         print('Inventory:\t', inv, bk, inv - bk)
+        print('Incoming order:\t', self.incoming_orders)
         print('Orders placed:\t', self.orders_placed)
         if self.week is not None and self.week < self.max_weeks:
             print('Next customer demand:\t', self.customer_demand[self.week])
+        if self._vec.full_table and self.week is not None:
+            table = self.shipments
+            print('Next shipments:\t', [(i, list(table[i])) for i in range(self.week + 1, self.week + 6)
+                                        if i < len(table)])
+        if self.week is not None:
+            print('Current delay:\t', self.shipment_delays[self.week])
         print('Inventory costs:\t', self.inventory_costs)
         print('Backlog costs:\t', self.backlog_costs)
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SCG_ABI_VERSION 3
+#define SCG_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define SCG_API __attribute__((visibility("default")))
@@ -103,6 +103,14 @@ typedef struct scg_bg_config {
   int32_t demand_lo, demand_hi;   /* SCG_DEMAND_UNIFORM: randint(lo, hi) per week (:77) */
   int32_t stochastic_delays;      /* v2: per-episode randint(delay_lo, delay_hi) (:91)  */
   int32_t delay_lo, delay_hi;
+  /* In (BeerGameEnv only): 1 = keep the reference's whole absolute-week shipment table
+   * instead of the ring — ring_slots becomes its row count max(T+1, max_w(w+d_w+1)) + 1
+   * (beergame_env.py:46-50), slot s holds week s, and shipments that land after the
+   * horizon are stored as the reference stores them. Rows are not cleared between
+   * episodes: a row not yet scheduled in the current episode holds a stale value (the
+   * reference's is 0; scg_bg_prepare's plan says which rows are scheduled by each week).
+   * Needs ring_slots <= 127. */
+  int32_t full_table;
 } scg_bg_config;
 
 /*
@@ -128,7 +136,8 @@ typedef struct scg_bg_state {
   /* Sticky DEVICE int32 error word (optional): bit 0 is set by any kernel whose int64
    * result (state, pipeline row, ledger, observation or reward; the reference computes in
    * int64, beergame_env.py:33,35,130-132) does not fit the int32 it is stored in. The
-   * stored values are then invalid; the flag stays set until the caller clears it. */
+   * stored values are then invalid; the flag stays set (across auto-resets too) until
+   * scg_bg_reset, whose kernel clears it and error_host in stream order, or the caller. */
   int32_t* error_flags;
   /* Optional HOST-mapped int32 (pinned, device-accessible): every terminal-week launch copies
    * error_flags there as the launch starts, so a host can poll earlier episodes' overflow

@@ -81,6 +81,9 @@ def case_inputs(name, spec):
     return info, demand, actions, thr
 
 
+SHIP_ENVS = 8
+
+
 def run_reference(info, demand, actions):
     from gym_supplychain.envs import BeerGameEnv
     T, N, L = actions.shape
@@ -92,6 +95,11 @@ def run_reference(info, demand, actions):
     rec["backlog_costs"] = np.zeros((N, L), dtype=np.int64)
     rec["all_orders_placed"] = np.zeros((N, L, T + 1), dtype=np.int64)
     rec["past_horizon_raises"] = np.zeros(N, dtype=bool)
+    # the order slips of every week, and the whole absolute-week shipment table of the
+    # first SHIP_ENVS envs every week (beergame_env.py:46-52, :79-81)
+    rec["incoming_orders"] = np.zeros((T, N, L), dtype=np.int64)
+    ns = min(N, SHIP_ENVS)
+    rec["shipments"] = None
     for n in range(N):
         env_info = dict(info)
         env_info["customer_demand"] = [int(x) for x in demand[n]]
@@ -106,6 +114,11 @@ def run_reference(info, demand, actions):
             rec["inventory"][w, n] = env.inventory
             rec["backlog"][w, n] = env.backlog
             rec["orders_placed"][w, n] = env.orders_placed
+            rec["incoming_orders"][w, n] = env.incoming_orders
+            if n < ns:
+                if rec["shipments"] is None:
+                    rec["shipments"] = np.zeros((T, ns) + env.shipments.shape, dtype=np.int64)
+                rec["shipments"][w, n] = env.shipments
         rec["inventory_costs"][n] = env.inventory_costs
         rec["backlog_costs"][n] = env.backlog_costs
         rec["all_orders_placed"][n] = env.all_orders_placed

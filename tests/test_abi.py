@@ -191,3 +191,46 @@ def test_slab_layout():
     assert nat.lib.scg_bg_slab_layout(ctypes.byref(c), 77, 0, off) == 0                     # 77 * 4 % 4 == 0
     c.levels = 3
     assert nat.lib.scg_bg_slab_layout(ctypes.byref(c), 77, 0, off) == nat.SCG_ERR_INVALID
+
+
+def _prepare_full(delays, T, variant=1):
+    from gym_supplychain_amd import _native as nat
+    c = nat.BgConfig()
+    c.levels, c.max_weeks, c.full_table, c.variant = 4, T, 1, variant
+    d = (ctypes.c_int32 * (T + 1))(*delays)
+    dem = (ctypes.c_int32 * T)(*([8] * T))
+    plan = (ctypes.c_int32 * (T + 1))()
+    c.shipment_delays, c.customer_demand = ctypes.cast(d, ctypes.c_void_p), ctypes.cast(dem, ctypes.c_void_p)
+    c.plan = ctypes.cast(plan, ctypes.c_void_p)
+    return nat.lib.scg_bg_prepare(ctypes.byref(c)), list(plan), c.ring_slots
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_prepare_full_table(seed):
+    """full_table: R = the reference's row count max(T+1, max_w(w+d_w+1)) + 1
+    (beergame_env.py:46-50), slot s = week s, and the weeks that ship past the horizon are
+    stored (STORE/ADD into rows > T) instead of dropped."""
+    from oracle.beergame import shipment_rows
+    rng = np.random.RandomState(100 + seed)
+    T = int(rng.randint(1, 40))
+    delays = [2] + rng.randint(0, 1 + int(rng.randint(1, 9)), size=T).tolist()
+    rc, plan, R = _prepare_full(delays, T)
+    assert rc == 0 and R == shipment_rows(T, np.asarray(delays))
+    written = set(range(1, delays[0] + 1))   # the initial pipeline, even past T (:52)
+    for w in range(1, T + 1):
+        d = delays[w]
+        mode = plan[w] & 3
+        assert (plan[w] >> 8) & 0xFF == d and bool(plan[w] & 4) == (w in written)
+        if d == 0:
+            assert mode == 0
+        else:
+            assert mode == (2 if w + d in written else 1), (w, d)
+            written.add(w + d)
+
+
+def test_prepare_full_table_limits():
+    from gym_supplychain_amd import _native as nat
+    rc, _, _ = _prepare_full([2] * 130, 129)             # 132 rows > 127
+    assert rc == nat.SCG_ERR_INVALID and "127" in nat.last_error()
+    rc, _, _ = _prepare_full([2] * 36, 35, variant=2)
+    assert rc == nat.SCG_ERR_INVALID and "full_table" in nat.last_error()

@@ -41,6 +41,9 @@ def test_single_env_oracle_matches_reference(name):
             obs, r, done, info = env.step(g["actions"][w, n].astype(np.int64))
             assert np.array_equal(obs, g["ref_obs"][w, n])
             assert r == g["ref_reward"][w, n] and done == g["ref_done"][w, n] and info == {}
+            assert np.array_equal(env.incoming_orders, g["ref_incoming_orders"][w, n])
+            if n < g["ref_shipments"].shape[1]:   # the whole absolute-week table (:46-52)
+                assert np.array_equal(env.shipments, g["ref_shipments"][w, n])
         assert g["ref_past_horizon_raises"][n]
         with pytest.raises(IndexError):
             env.step(np.zeros(L, dtype=np.int64))
