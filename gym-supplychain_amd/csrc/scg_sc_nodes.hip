@@ -8,16 +8,26 @@
 // once, so the same work hides its latencies behind W times as many waves.
 //
 // LDS per block (doubles first): the block's heaps [NP][H][64], released sums [NP][64],
-// shipment inbox [E][64], node costs [NN][64], the stocks a step started from [NP][64]; then
-// the int32 heap times/kinds, heap sizes, inbox times/kinds, cost kinds and the per-wave
-// "order not provable" flags [W][64].
-//   stage  (wave w, its nodes)  heaps HBM -> LDS, released sums, flags
-//   act    (wave w, its nodes)  stock, costs, shipments -> inbox, stock obs | barrier
+// shipment inbox [E][64], node costs [NN][64], the observation tile [64][O|1] (float or
+// double); then the int32 heap times/kinds, heap sizes, inbox times/kinds, cost kinds, the
+// per-wave "order not provable" flags [W][64] and the action tile [64][A|1].
+//   stage  (wave w, its nodes)  heaps HBM -> LDS, released sums, flags; every thread
+//                               loads a share of the block's action rows (one contiguous
+//                               span) into the action tile                    | barrier
+//   act    (wave w, its nodes)  stock, costs, shipments -> inbox, stock obs   | barrier
 //   heaps  (wave w, its nodes)  inbox pushes, pops, supply push, bins, copy back
-//   reward (wave 0)             -(costs in node order), return, demand / time obs, reset
-// An env any wave flagged skips heaps; wave 0 puts its stocks back and steps it alone on its
-// staged heaps, node after node in the reference's order (sc_nodes_serial).
+//   reward (wave 0)             -(costs in node order), return, demand / time obs
+//                                                                             | barrier
+//   out    (every thread)       the observation tile -> HBM, one contiguous span per block;
+//                               wave 0 resets its envs at an auto-reset step
+// An env any wave flagged skips act and heaps; wave 0 steps it alone on its staged heaps,
+// node after node in the reference's order (sc_nodes_serial). Observations and actions go
+// through LDS tiles so HBM sees whole rows; the state pointers stay the batch's base
+// pointers (ScEnv soff/hoff) so they live in SGPRs.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <type_traits>
 
 #include "scg_common.h"
 #include "scg_supplychain_core.h"
@@ -52,67 +62,76 @@ constexpr int kNodesMaxWaves = 8;
 #endif
 // Four waves per SIMD (<= 128 VGPRs): two blocks of eight waves per CU, which is also what
 // their LDS allows.
-template <int MAXD>
+template <int MAXD, bool F64>
 __global__ __launch_bounds__(64 * kNodesMaxWaves) __attribute__((amdgpu_waves_per_eu(SCG_NODES_WPE)))
 void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
+  using ObsT = typename std::conditional<F64, double, float>::type;
   extern __shared__ __align__(16) unsigned char smem[];
   const ScCtx& c = a.c;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t n = static_cast<int64_t>(blockIdx.x) * 64 + lane;
-  const bool live = n < a.n;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t n = n0 + lane;
+  const int nb = a.n - n0 < 64 ? static_cast<int>(a.n - n0) : 64;  // envs of this block
+  const bool live = lane < nb;
   const int NN = c.n_nodes, P = c.P, NP = NN * P, H = c.H;
+  const int Ap = c.A | 1, Op = c.O | 1;  // odd row strides: lanes hit distinct banks
   double* hval = reinterpret_cast<double*>(smem);
   double* recv = hval + static_cast<int64_t>(NP) * H * 64;
   double* ibval = recv + NP * 64;
   double* cost_v = ibval + static_cast<int64_t>(E) * 64;
-  double* stock0 = cost_v + NN * 64;
-  int32_t* htk = reinterpret_cast<int32_t*>(stock0 + NP * 64);
+  ObsT* obs_t = reinterpret_cast<ObsT*>(cost_v + NN * 64);
+  int32_t* htk = reinterpret_cast<int32_t*>(obs_t + 64 * Op);
   int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
   int32_t* ibtk = hsz + NP * 64;
   int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
   int32_t* amb = cost_k + NN * 64;
-  ScEnv g = env_view(a, n, a.episode);
+  float* act_t = reinterpret_cast<float*>(amb + W * 64);
+  ScEnv g{a.stock, a.tk, a.val, a.size, a.n, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
+  g.soff = n;
+  g.hoff = n;
   auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
   NSTAMP(0);
 
-  // node observations go to obs, or to the terminal observation when the env resets now
-  const bool terminal = a.flags & 1;
-  const bool autoreset = a.flags & 2;
-  void* node_obs = autoreset ? a.term_obs : a.obs;
-  ObsRow main{node_obs ? node_obs : a.obs, n * c.O, a.obs_f64};
-  ObsRow extra{a.term_obs, n * c.O, a.obs_f64};
-  const bool both = terminal && !autoreset && a.term_obs;
-  auto sink = [&](int o, double x) {
-    if (node_obs) main(o, x);
-    if (both) extra(o, x);
-  };
+  // the step's observation row, whichever buffer(s) it goes to (chosen at the copy-out)
+  ObsT* const orow = obs_t + lane * Op;
+  auto sink = [&](int o, double x) { orow[o] = static_cast<ObsT>(x); };
   const NodesInbox in{ibtk + lane, ibval + lane, 64};
-  const float* act = a.act + n * c.A;
+  const float* act = act_t + lane * Ap;
 
-  // stage, then act at once (no barrier between): a node's act needs only what its own heaps
-  // release. The stock it starts from is kept, so an env some wave flags is put back and
-  // stepped by the serial walk below.
+  // stage: every heap of the wave's nodes, and the block's action rows into the tile
+  {
+    const float* src = a.act + n0 * c.A;
+    const int total = nb * c.A;
+    for (int q = threadIdx.x; q < total; q += blockDim.x) {
+      const int r = q / c.A;
+      act_t[r * Ap + (q - r * c.A)] = src[q];
+    }
+  }
   bool bad = false;
   if (live)
-    for (int i = w; i < NN; i += W) {
+    for (int i = w; i < NN; i += W)
       for (int p = 0; p < P; ++p) {
         const int hp = i * P + p;
-        stock0[hp * 64 + lane] = a.stock[hp * a.n + n];
         bad |= !sc_nodes_stage(c, g, lheap(hp), hsz[hp * 64 + lane], a.t, i, p, recv[hp * 64 + lane]);
       }
-      NSTAMP(5);  // (the last node of the wave's) heaps staged, act next
+  amb[w * 64 + lane] = bad ? 1 : 0;
+  NSTAMP(5);
+  __syncthreads();
+  bool flagged = (a.flags & 4) != 0;
+  for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
+  const bool go = live && !flagged;
+
+  // act: every node at once (a node's act needs only what its own heaps release)
+  if (go)
+    for (int i = w; i < NN; i += W) {
       const Num cst = sc_nodes_act<MAXD>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
       cost_v[i * 64 + lane] = cst.v;
       cost_k[i * 64 + lane] = cst.k;
       for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
     }
-  amb[w * 64 + lane] = bad ? 1 : 0;
   NSTAMP(1);
   __syncthreads();
   NSTAMP(2);
-  bool flagged = (a.flags & 4) != 0;
-  for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
-  const bool go = live && !flagged;
 
   // heaps
   if (go)
@@ -125,13 +144,13 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
       }
     }
   NSTAMP(3);
-  if (autoreset) __syncthreads();  // the reset below rewrites heaps the other waves store
 
   // reward
+  const bool terminal = a.flags & 1;
+  const bool autoreset = a.flags & 2;
   if (w == 0 && live) {
     double reward;
-    if (flagged) {  // its stocks back as they were; no wave touched its heaps: they are as staged
-      for (int hp = 0; hp < NP; ++hp) a.stock[hp * a.n + n] = stock0[hp * 64 + lane];
+    if (flagged) {  // untouched by act and heaps: the serial walk on its staged heaps
       reward = sc_nodes_serial<MAXD>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
     } else {
       Num total = pyint(0);
@@ -144,29 +163,37 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
       if (terminal && a.final_ret) a.final_ret[n] = r;
       a.ep_ret[n] = autoreset ? 0.0 : r;
     }
-    auto rest = [&](ObsRow& row, int t) {  // demand and time-to-go elements (:771, :786)
-      for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, t, k, row);
-      sc_observe_tail(c, t, row);
-    };
-    if (autoreset) {
-      if (a.term_obs) rest(extra, a.t);
-      g.episode = a.episode + 1;
-      sc_reset_env(c, g);
-      ObsRow out{a.obs, n * c.O, a.obs_f64};
-      sc_observe(c, g, 0, out);
-    } else {
-      rest(main, a.t);
-      if (both) rest(extra, a.t);
-    }
+    for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, a.t, k, sink);  // (:771)
+    sc_observe_tail(c, a.t, sink);                                               // (:786)
+  }
+  __syncthreads();
+
+  // out: the tile is this step's observation — obs, or the terminal observation when the
+  // env resets now (then wave 0 writes the reset observation to obs), or both
+  ObsT* const dst0 = static_cast<ObsT*>(autoreset ? a.term_obs : a.obs);
+  ObsT* const dst1 = (terminal && !autoreset) ? static_cast<ObsT*>(a.term_obs) : nullptr;
+  const int cells = nb * c.O;
+  for (int q = threadIdx.x; q < cells; q += blockDim.x) {
+    const int r = q / c.O;
+    const ObsT x = obs_t[r * Op + (q - r * c.O)];
+    if (dst0) dst0[n0 * c.O + q] = x;
+    if (dst1) dst1[n0 * c.O + q] = x;
+  }
+  if (autoreset && w == 0 && live) {  // after the barrier: every wave's heap copy-back landed
+    g.episode = a.episode + 1;
+    sc_reset_env(c, g);
+    ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
+    sc_observe(c, g, 0, out);
   }
   if (live && g.overflow) atomicOr(a.err, 1);
   NSTAMP(4);
 }
 
-// LDS bytes of one block (the layout above).
-size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W) {
+// LDS bytes of one block (the layout above); obs_bytes 4 (float) or 8 (double).
+size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W, int A, int O, int obs_bytes) {
   const size_t NP = static_cast<size_t>(n_nodes) * P;
-  return 64 * ((NP * H + 2 * NP + E + n_nodes) * 8 + (NP * H + NP + E + n_nodes + W) * 4);
+  return 64 * ((NP * H + NP + E + n_nodes) * 8 + static_cast<size_t>(O | 1) * obs_bytes +
+               (NP * H + NP + E + n_nodes + W) * 4 + static_cast<size_t>(A | 1) * 4);
 }
 
 // Widest destination list the kernel is instantiated for (its split runs in registers).
@@ -175,34 +202,48 @@ int sc_nodes_max_dests() { return 8; }
 // Waves per block for a chain: one per node up to kNodesMaxWaves.
 int sc_nodes_waves(int n_nodes) { return n_nodes < kNodesMaxWaves ? n_nodes : kNodesMaxWaves; }
 
-// A block may hold up to the CU's whole LDS (gfx950: 160 KiB); past 64 KiB the kernel is
-// told once that it may.
-constexpr size_t kNodesLdsMax = 160 * 1024;
-size_t sc_nodes_lds_max() { return kNodesLdsMax; }
+// A block may use up to the CU's whole LDS (gfx950: 160 KiB; asked of the device once, the
+// gfx950 figure when no device answers, e.g. scg_sc_prepare on a host without a GPU); past
+// 64 KiB the kernel is told once per device that it may.
+constexpr size_t kNodesLdsGfx950 = 160 * 1024;
+size_t sc_nodes_lds_max() {
+  static std::atomic<size_t> cached{0};
+  size_t v = cached.load(std::memory_order_relaxed);
+  if (v) return v;
+  int dev = 0, bytes = 0;
+  v = (hipGetDevice(&dev) == hipSuccess &&
+       hipDeviceGetAttribute(&bytes, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) == hipSuccess && bytes > 0)
+          ? static_cast<size_t>(bytes)
+          : kNodesLdsGfx950;
+  cached.store(v, std::memory_order_relaxed);
+  return v;
+}
 
-template <int MAXD>
+template <int MAXD, bool F64>
 int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
-  static bool raised[64] = {};  // per device; setting it twice from racing threads is harmless
-  const size_t lds = sc_nodes_lds_bytes(a.c.n_nodes, a.c.P, a.c.H, E, W);
+  static std::atomic<bool> raised[64] = {};  // per device
+  const size_t lds = sc_nodes_lds_bytes(a.c.n_nodes, a.c.P, a.c.H, E, W, a.c.A, a.c.O, F64 ? 8 : 4);
+  if (lds > sc_nodes_lds_max()) return fail(SCG_ERR_INVALID, "node-parallel kernel: %zu B of LDS per block", lds);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (lds > 64 * 1024 && !raised[dev]) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sc_step_nodes_kernel<MAXD>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNodesLdsMax)) != hipSuccess)
+  if (lds > 64 * 1024 && !raised[dev].load(std::memory_order_acquire)) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sc_step_nodes_kernel<MAXD, F64>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sc_nodes_lds_max())) != hipSuccess)
       return fail(SCG_ERR_HIP, "node-parallel kernel: cannot raise its LDS limit");
-    raised[dev] = true;
+    raised[dev].store(true, std::memory_order_release);
   }
-  hipLaunchKernelGGL(sc_step_nodes_kernel<MAXD>, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64 * W), lds, s,
-                     a, W, E);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_nodes_kernel<MAXD, F64>), dim3(static_cast<unsigned>((a.n + 63) / 64)),
+                     dim3(64 * W), lds, s, a, W, E);
   return check_launch("sc_step_nodes_kernel");
 }
 
 int sc_launch_nodes(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t s) {
   if (W < 1 || W > kNodesMaxWaves) return fail(SCG_ERR_INVALID, "node-parallel kernel: %d waves per block", W);
+  const bool f64 = a.obs_f64 != 0;
   switch (maxd_bucket) {
-    case 2: return sc_launch_nodes_d<2>(a, W, E, s);
-    case 4: return sc_launch_nodes_d<4>(a, W, E, s);
-    case 8: return sc_launch_nodes_d<8>(a, W, E, s);
+    case 2: return f64 ? sc_launch_nodes_d<2, true>(a, W, E, s) : sc_launch_nodes_d<2, false>(a, W, E, s);
+    case 4: return f64 ? sc_launch_nodes_d<4, true>(a, W, E, s) : sc_launch_nodes_d<4, false>(a, W, E, s);
+    case 8: return f64 ? sc_launch_nodes_d<8, true>(a, W, E, s) : sc_launch_nodes_d<8, false>(a, W, E, s);
     default: return fail(SCG_ERR_INVALID, "node-parallel kernel: nodes ship to at most 8 destinations");
   }
 }

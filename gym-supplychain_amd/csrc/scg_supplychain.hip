@@ -74,7 +74,7 @@ struct ScAcc {
 namespace scg {
 
 // scg_sc_nodes.hip
-size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W);
+size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W, int A, int O, int obs_bytes);
 int sc_nodes_waves(int n_nodes);
 int sc_nodes_max_dests();
 size_t sc_nodes_lds_max();
@@ -687,7 +687,8 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   if (want == SCG_SC_KERNEL_AUTO && NN <= sc_nodes_waves(NN) && maxd <= sc_nodes_max_dests() && H <= 64) {
     std::vector<scg_sc_node> probe(nodes, nodes + NN);
     const int entries = sc_inbox_layout(cfg, probe.data());
-    if (entries >= 0 && 2 * sc_nodes_lds_bytes(NN, P, H, entries, sc_nodes_waves(NN)) <= sc_nodes_lds_max())
+    if (entries >= 0 && 2 * sc_nodes_lds_bytes(NN, P, H, entries, sc_nodes_waves(NN), n_act, cfg->n_obs,
+                                               cfg->obs_f64 ? 8 : 4) <= sc_nodes_lds_max())
       want = SCG_SC_KERNEL_NODES;
   }
   if (want == SCG_SC_KERNEL_AUTO && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
@@ -701,7 +702,7 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
     const int W = sc_nodes_waves(NN);
     if (maxd > sc_nodes_max_dests())
       return fail(SCG_ERR_INVALID, "the node-parallel kernel takes nodes with at most %d destinations", sc_nodes_max_dests());
-    if (H > 64 || sc_nodes_lds_bytes(NN, P, H, entries, W) > sc_nodes_lds_max())
+    if (H > 64 || sc_nodes_lds_bytes(NN, P, H, entries, W, n_act, cfg->n_obs, cfg->obs_f64 ? 8 : 4) > sc_nodes_lds_max())
       return fail(SCG_ERR_INVALID, "a block's heaps and inbox (%d nodes x %d products x %d slots, %d entries) exceed "
                   "the node-parallel kernel's LDS", NN, P, H, entries);
     cfg->inbox_size = entries;

@@ -93,6 +93,12 @@ struct ScEnv {
   int64_t led_stride = 0;
   int32_t hnode0 = 0;  // first node whose heaps the heap arrays hold (staged kernel: the current one)
   ScAcc* dbg = nullptr;  // diagnostic builds only (SCG_ACCP)
+  // Element offset of this env added to every stock / ledger index (soff) and heap / size
+  // index (hoff): 0 when the pointers above already point at the env's first element; the
+  // env's column when they are the batch's base pointers (node-parallel kernel), which keeps
+  // them wave-uniform (SGPRs) instead of one 64-bit VGPR pair per pointer and lane.
+  int64_t soff = 0;
+  int64_t hoff = 0;
 };
 
 // info['sc_episode'] categories in the reference's dict order (:416-417)
@@ -107,8 +113,8 @@ enum ScLedgerKey : int {
 // change neither value nor type of a sum, so they are skipped.
 __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int key, int p, Num cost, Num units) {
   if (!e.led_v) return;
-  const int64_t i0 = (static_cast<int64_t>(key) * c.P + p) * e.led_stride;
-  const int64_t i1 = (static_cast<int64_t>(SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride;
+  const int64_t i0 = (static_cast<int64_t>(key) * c.P + p) * e.led_stride + e.soff;
+  const int64_t i1 = (static_cast<int64_t>(SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride + e.soff;
   const Num a = np_add(Num{e.led_v[i0], np_kind_int(e.led_k[i0])}, cost);
   const Num b = np_add(Num{e.led_v[i1], np_kind_int(e.led_k[i1])}, units);
   e.led_v[i0] = a.v;
@@ -121,22 +127,22 @@ __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int k
 __host__ __device__ inline void sc_reset_ledger(const ScCtx& c, ScEnv& e) {
   if (!e.led_v) return;
   for (int q = 0; q < 2 * SCG_SC_LEDGER_KEYS * c.P; ++q) {
-    e.led_v[q * e.led_stride] = 0.0;
-    e.led_k[q * e.led_stride] = np_kind_abi(NK_INT);
+    e.led_v[q * e.led_stride + e.soff] = 0.0;
+    e.led_k[q * e.led_stride + e.soff] = np_kind_abi(NK_INT);
   }
 }
 
 __host__ __device__ __forceinline__ HeapView sc_heap(const ScCtx& c, const ScEnv& e, int node, int p) {
   const int64_t hp = static_cast<int64_t>(node - e.hnode0) * c.P + p;
-  return HeapView{e.tk + hp * c.H * e.hstride, e.val + hp * c.H * e.hstride, e.hstride};
+  return HeapView{e.tk + hp * c.H * e.hstride + e.hoff, e.val + hp * c.H * e.hstride + e.hoff, e.hstride};
 }
 
 __host__ __device__ __forceinline__ int32_t& sc_size(const ScCtx& c, const ScEnv& e, int node, int p) {
-  return e.size[(static_cast<int64_t>(node - e.hnode0) * c.P + p) * e.hstride];
+  return e.size[(static_cast<int64_t>(node - e.hnode0) * c.P + p) * e.hstride + e.hoff];
 }
 
 __host__ __device__ __forceinline__ double& sc_stock(const ScCtx& c, const ScEnv& e, int node, int p) {
-  return e.stock[(static_cast<int64_t>(node) * c.P + p) * e.stride];
+  return e.stock[(static_cast<int64_t>(node) * c.P + p) * e.stride + e.soff];
 }
 
 // Philox word cache: consecutive words of one (env, episode, stream) come 4 per call.
