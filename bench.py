@@ -82,15 +82,30 @@ def step_bytes_per_env(plan_word, week, T, L, ring_initial_slots, ledgers, histo
     return b
 
 
+def profile_tag_key(path):
+    """Sort key of a profiles/ file by its session tag rNN<letters>: round number, then the
+    letters as a bijective base-26 count (a..z, aa..az, ...), so r02al is newer than r02z."""
+    import re
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    if not m:
+        return (-1, -1)
+    n = 0
+    for ch in m.group(2):
+        n = n * 26 + (ord(ch) - ord("a") + 1)
+    return (int(m.group(1)), n)
+
+
 def pmc_traffic(kernel_substr=KERNEL, n_envs=N_ENVS):
-    """HBM bytes per launch of the step kernel from the latest committed PMC summary that
+    """HBM bytes per launch of the step kernel from the newest committed PMC summary that
     has it (profiles/rNN*_pmc_summary.json, tools/pmc_summary.py, separate rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes of this bench at 65,536 envs; FETCH_SIZE doubled per
-    MI355X_MICROARCH.md §HBM). None when absent or for another batch size."""
+    MI355X_MICROARCH.md §HBM, calibrated for this repo's access shapes in
+    profiles/r03b_pmc_calib_*.csv). None when absent or for another batch size."""
     import glob
     if n_envs != N_ENVS:
         return None, None
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), key=profile_tag_key,
+                       reverse=True):
         with open(path) as f:
             traffic = json.load(f).get("traffic", {})
         for name, t in traffic.items():
@@ -225,7 +240,7 @@ def stream_copy_peak(device, nbytes=1 << 30, iters=20):
     src = torch.empty(nbytes // 4, dtype=torch.int32, device=device).fill_(7)
     dst = torch.empty_like(src)
     stream = torch.cuda.current_stream(device)
-    blocks = 256 * 32      # 32 workgroups (128 waves) per CU over the copy, 4 loads in flight per lane
+    blocks = 0             # one 16-byte vector per lane over the whole buffer (profiles/r03b_copy_probe.log)
 
     def copy():
         nat.check(nat.lib.scg_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, blocks,
@@ -283,7 +298,7 @@ def beyond_cache_point(device, n_envs=BEYOND_CACHE_ENVS, episodes=2):
             "env_steps_per_s_gpu": n_envs * k / (ms / 1e3)}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3500)
@@ -296,37 +311,103 @@ def main():
                     help="launches timed one at a time with kernel-stamped events after the timed region")
     ap.add_argument("--no-dry-region", action="store_true",
                     help="skip the untimed K-step region (sync, K steps, sync) run right before the timed one")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
-    torch.cuda.set_device(device)
+class Platform:
+    """What the measurement flow needs from the machine: the rank layout, the batch env and
+    its resident week actions, the collective device, synchronisation and kernel-stamped
+    events. GpuPlatform is the real one; tests/test_bench_distributed.py runs the same flow
+    (run()) on gloo ranks with a CPU stand-in."""
+    world, rank, device = 1, 0, None
 
-    import ctypes
+    def make_env(self, n_envs, env_offset):
+        raise NotImplementedError
 
-    from gym_supplychain_amd import BeerGameVecEnv
-    from gym_supplychain_amd import _native as nat
+    def week_actions(self, env, n_envs):
+        raise NotImplementedError
+
+    def sync(self):
+        pass
+
+    def barrier(self):
+        import torch.distributed as dist
+        dist.barrier()
+
+    def new_event(self):
+        raise NotImplementedError
+
+    def elapsed_ms(self, start, stop):
+        raise NotImplementedError
+
+    def destroy_event(self, ev):
+        pass
+
+    def extras(self):
+        return {}
+
+    def cpu_baseline(self, budget):
+        return cpu_baseline(budget)
+
+
+class GpuPlatform(Platform):
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        self.device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(self.device)
+        from gym_supplychain_amd import _native as nat
+        self.nat = nat
+
+    def make_env(self, n_envs, env_offset):
+        from gym_supplychain_amd import BeerGameVecEnv
+        return BeerGameVecEnv(n_envs, {}, demand="poisson", poisson_lambda=LAMBDA, seed=SEED, device=self.device,
+                              env_offset=env_offset, auto_reset=True, track_costs=True, track_history=True,
+                              track_returns=True)
+
+    def week_actions(self, env, n_envs):
+        import ctypes
+
+        import torch
+        stream = torch.cuda.current_stream(self.device)
+        actions = torch.empty((WEEKS, n_envs, LEVELS), dtype=torch.int32, device=self.device)
+        self.nat.check(self.nat.lib.scg_uniform_ints(SEED, env.env_offset, n_envs, WEEKS, LEVELS, 0, 0, 8,
+                                                     actions.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        return list(actions.unbind(0))  # the policy output of each week, resident in HBM
+
+    def sync(self):
+        import torch
+        torch.cuda.synchronize(self.device)
+
+    def new_event(self):
+        return self.nat.hip_event()
+
+    def elapsed_ms(self, start, stop):
+        return self.nat.hip_event_elapsed_ms(start, stop)
+
+    def destroy_event(self, ev):
+        self.nat.hip_event_destroy(ev)
+
+    def extras(self):
+        return {"measured_peak": stream_copy_peak(self.device), "beyond_cache": beyond_cache_point(self.device)}
+
+
+def run(args, plat):
+    """The measurement flow of every rank (module docstring); returns rank 0's JSON line as
+    a dict (None on other ranks)."""
     from gym_supplychain_amd.distributed import EpisodeReturnGather, shard_offset
-
+    world, rank, device = plat.world, plat.rank, plat.device
     N = args.envs
-    env = BeerGameVecEnv(N, {}, demand="poisson", poisson_lambda=LAMBDA, seed=SEED, device=device,
-                         env_offset=shard_offset(N, rank), auto_reset=True, track_costs=True,
-                         track_history=True, track_returns=True)
-    stream = torch.cuda.current_stream(device)
-    actions = torch.empty((WEEKS, N, LEVELS), dtype=torch.int32, device=device)
-    nat.check(nat.lib.scg_uniform_ints(SEED, env.env_offset, N, WEEKS, LEVELS, 0, 0, 8, actions.data_ptr(),
-                                       ctypes.c_void_p(stream.cuda_stream)))
+    env = plat.make_env(N, shard_offset(N, rank))
     gather = EpisodeReturnGather(N, device)
     env.reset()
-    loop = StepLoop(env, list(actions.unbind(0)), gather)  # the policy output of each week, resident in HBM
+    loop = StepLoop(env, plat.week_actions(env, N), gather)
     plan = list(env._plan)
 
     def week_bytes(w):
@@ -336,87 +417,95 @@ def main():
         w0 = env.week
         return sum(week_bytes((w0 + i) % WEEKS + 1) for i in range(k))
 
-    def sync():
-        torch.cuda.synchronize(device)
-
-    barrier = dist.barrier if world > 1 else None
-    ev = [nat.hip_event() for _ in range(4)]
+    barrier = plat.barrier if world > 1 else None
+    ev = [plat.new_event() for _ in range(4)]
 
     warmup_run = max(args.warmup, WEEKS)
     loop.run(warmup_run)
     if not args.no_dry_region:  # one untimed region of the same shape (sync, K steps, sync) right
-        region(loop, args.steps, world, barrier, sync)  # before: 7.9e9-9.8e9 -> 1.01e10-1.04e10 at K = 20
-        warmup_run += args.steps                        # (profiles/r02m_dry_region.log)
+        region(loop, args.steps, world, barrier, plat.sync)  # before: 7.9e9-9.8e9 -> 1.01e10-1.04e10 at K = 20
+        warmup_run += args.steps                             # (profiles/r02m_dry_region.log)
     import gc
     gc.disable()  # no collector pass inside a timed region
-    # headline: exactly K steps
-    elapsed, _ = region(loop, args.steps, world, barrier, sync)  # unstamped (profiles/r02s_stamped_headline_ab.log)
-    gather.result()
-    # 100 whole episodes, from an episode boundary
-    loop.run((WEEKS - env.week) % WEEKS)
-    k_ep = EPISODES_TIMED * WEEKS
-    ep_bytes = bytes_of(k_ep)
-    ep_elapsed, ep_gpu_ms = region(loop, k_ep, world, barrier, sync, (ev[2], ev[3], nat.hip_event_elapsed_ms))
-    gather.result()
-    # isolated launches: whole 35-week cycles, each stamped and run alone
-    k_samples = max(WEEKS, args.kernel_samples // WEEKS * WEEKS)
-    sampled_bytes = bytes_of(k_samples)
-    iso = [(nat.hip_event(), nat.hip_event()) for _ in range(k_samples)]
-    loop.run(k_samples, each=iso, sync_each=sync)
-    iso_ms = sum(nat.hip_event_elapsed_ms(s, e) for s, e in iso)
+    try:
+        # headline: exactly K steps, unstamped (profiles/r02s_stamped_headline_ab.log)
+        elapsed, _ = region(loop, args.steps, world, barrier, plat.sync)
+        gather.result()
+        # 100 whole episodes, from an episode boundary
+        loop.run((WEEKS - env.week) % WEEKS)
+        k_ep = EPISODES_TIMED * WEEKS
+        ep_bytes = bytes_of(k_ep)
+        ep_elapsed, ep_gpu_ms = region(loop, k_ep, world, barrier, plat.sync, (ev[2], ev[3], plat.elapsed_ms))
+        gather.result()
+        # isolated launches: whole 35-week cycles, each stamped and run alone
+        k_samples = max(WEEKS, args.kernel_samples // WEEKS * WEEKS)
+        sampled_bytes = bytes_of(k_samples)
+        iso = [(plat.new_event(), plat.new_event()) for _ in range(k_samples)]
+        loop.run(k_samples, each=iso, sync_each=plat.sync)
+        iso_ms = sum(plat.elapsed_ms(a, b) for a, b in iso)
+    finally:
+        gc.enable()
     for e in ev + [x for pair in iso for x in pair]:
-        nat.hip_event_destroy(e)
+        plat.destroy_event(e)
     env.check_errors()
     elapsed, ep_elapsed, ep_gpu_ms, iso_ms = max_over_ranks([elapsed, ep_elapsed, ep_gpu_ms, iso_ms], world, device)
-    extras = {}
-    if rank == 0 and world == 1 and not args.no_extras:
-        extras["measured_peak"] = stream_copy_peak(device)
-        extras["beyond_cache"] = beyond_cache_point(device)
+    extras = plat.extras() if rank == 0 and world == 1 and not args.no_extras else {}
+    if rank != 0:
+        return None
+    achieved = ep_bytes / (ep_gpu_ms / 1e3) / 1e9
+    traffic, traffic_src = pmc_traffic(n_envs=N)
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": f"scg::{KERNEL} (L = 4, Poisson demand, state slab)",
+            "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
+            "avg_kernel_source": "the 100-episode timed region: first launch's dispatch begin to last launch's "
+                                 "end (hipExtLaunchKernel stamps, nothing stamped in between) / launches",
+            "bytes_per_launch": ep_bytes / k_ep, "launches_timed": k_ep,
+            "isolated_kernel_us": iso_ms * 1e3 / k_samples, "isolated_launches": k_samples,
+            "isolated_frac": sampled_bytes / (iso_ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    if "measured_peak" in extras:
+        roof["measured_peak"] = extras["measured_peak"]
+        roof["frac_measured_peak"] = achieved / extras["measured_peak"]
+        roof["measured_peak_source"] = ("scg_stream_copy of 1 GiB (read + write; one non-temporal 16-B "
+                                        "vector per lane), 20 launches, same run")
+        roof["beyond_cache"] = extras["beyond_cache"]
+    line = {
+        "metric": "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X",
+        "value": N * world * args.steps / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "warmup_steps_run": warmup_run,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: Poisson(8) demand drawn on device (Philox4x32-10), uniform int [0,8] actions",
+        "config": {"workload": "beergame-v0 step() x 65536 envs/GPU (BASELINE configs[1]; configs[4] at N=8)",
+                   "n_envs_per_gpu": N, "levels": LEVELS, "weeks": WEEKS, "auto_reset": True,
+                   "ledgers": True, "orders_history": True, "episode_return_allgather": world > 1,
+                   "parallelism": f"env-shard x{world}"},
+        "episodes_timed": {"episodes": EPISODES_TIMED, "steps": k_ep, "value": N * world * k_ep / ep_elapsed,
+                           "ms_per_step": ep_elapsed * 1e3 / k_ep, "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
+                           "frac": ep_bytes / (ep_gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+        "roofline": roof,
+        "episode_returns_gathered": gather.gathers,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = plat.cpu_baseline(args.cpu_budget)
+    return line
 
-    if rank == 0:
-        achieved = ep_bytes / (ep_gpu_ms / 1e3) / 1e9
-        traffic, traffic_src = pmc_traffic(n_envs=N)
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": f"scg::{KERNEL} (L = 4, Poisson demand, state slab)",
-                "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
-                "avg_kernel_source": "the 100-episode timed region: first launch's dispatch begin to last launch's "
-                                     "end (hipExtLaunchKernel stamps, nothing stamped in between) / launches",
-                "bytes_per_launch": ep_bytes / k_ep, "launches_timed": k_ep,
-                "isolated_kernel_us": iso_ms * 1e3 / k_samples, "isolated_launches": k_samples,
-                "isolated_frac": sampled_bytes / (iso_ms / 1e3) / 1e9 / HBM_PEAK_GBS}
-        if "measured_peak" in extras:
-            roof["measured_peak"] = extras["measured_peak"]
-            roof["frac_measured_peak"] = achieved / extras["measured_peak"]
-            roof["measured_peak_source"] = "scg_stream_copy of 1 GiB (read + write), 20 launches, same run"
-            roof["beyond_cache"] = extras["beyond_cache"]
-        line = {
-            "metric": "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X",
-            "value": N * world * args.steps / elapsed,
-            "unit": "env-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "warmup_steps_run": warmup_run,
-            "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int32",
-            "data": "synthetic: Poisson(8) demand drawn on device (Philox4x32-10), uniform int [0,8] actions",
-            "config": {"workload": "beergame-v0 step() x 65536 envs/GPU (BASELINE configs[1]; configs[4] at N=8)",
-                       "n_envs_per_gpu": N, "levels": LEVELS, "weeks": WEEKS, "auto_reset": True,
-                       "ledgers": True, "orders_history": True, "episode_return_allgather": world > 1,
-                       "parallelism": f"env-shard x{world}"},
-            "episodes_timed": {"episodes": EPISODES_TIMED, "steps": k_ep, "value": N * world * k_ep / ep_elapsed,
-                               "ms_per_step": ep_elapsed * 1e3 / k_ep, "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
-                               "frac": ep_bytes / (ep_gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
-            "roofline": roof,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+
+def main(argv=None):
+    args = parse_args(argv)
+    plat = GpuPlatform()
+    line = run(args, plat)
+    if line is not None:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if plat.world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -35,8 +35,8 @@
 #include "scg_supplychain_nodes.h"
 
 // Diagnostic build only (-DSCG_NODES_STAMPS, tools/nodes_stamps.py): lane 0 of every wave
-// records the shader clock at the phase boundaries (0 start, 5 heaps staged, 1 acted, 2 past
-// the barrier, 3 heaps done, 4 end) into a buffer of its own that scg_nodes_debug_stamps copies
+// records the shader clock at the phase boundaries (0 start, 5 heaps staged, 6 past the first
+// barrier, 1 acted, 2 past the second, 3 heaps done, 7 past the third, 4 end) into a buffer of its own that scg_nodes_debug_stamps copies
 // out; nothing else reads it. In the product build NSTAMP is empty.
 #ifdef SCG_NODES_STAMPS
 constexpr int kNStampSlots = 8;
@@ -79,15 +79,18 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   double* recv = hval + static_cast<int64_t>(NP) * H * 64;
   double* ibval = recv + NP * 64;
   double* cost_v = ibval + static_cast<int64_t>(E) * 64;
-  ObsT* obs_t = reinterpret_cast<ObsT*>(cost_v + NN * 64);
+  double* stk = cost_v + NN * 64;  // the block's stocks [NP][64] for the step
+  double* ret0 = stk + NP * 64;    // episode returns [64] (wave 0's prefetch)
+  ObsT* obs_t = reinterpret_cast<ObsT*>(ret0 + 64);
   int32_t* htk = reinterpret_cast<int32_t*>(obs_t + 64 * Op);
   int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
   int32_t* ibtk = hsz + NP * 64;
   int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
   int32_t* amb = cost_k + NN * 64;
   float* act_t = reinterpret_cast<float*>(amb + W * 64);
-  ScEnv g{a.stock, a.tk, a.val, a.size, a.n, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
-  g.soff = n;
+  // heaps and sizes in HBM (the batch's base pointers, column n); stocks in the LDS copy
+  ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
+  g.soff = lane;
   g.hoff = n;
   auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
   NSTAMP(0);
@@ -108,15 +111,19 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
     }
   }
   bool bad = false;
-  if (live)
+  if (live) {
     for (int i = w; i < NN; i += W)
       for (int p = 0; p < P; ++p) {
         const int hp = i * P + p;
+        stk[hp * 64 + lane] = a.stock[hp * a.n + n];
         bad |= !sc_nodes_stage(c, g, lheap(hp), hsz[hp * 64 + lane], a.t, i, p, recv[hp * 64 + lane]);
       }
+    if (w == 0 && a.ep_ret) ret0[lane] = a.ep_ret[n];
+  }
   amb[w * 64 + lane] = bad ? 1 : 0;
   NSTAMP(5);
   __syncthreads();
+  NSTAMP(6);
   bool flagged = (a.flags & 4) != 0;
   for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
   const bool go = live && !flagged;
@@ -159,7 +166,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
     }
     a.rew[n] = reward;
     if (a.ep_ret) {
-      const double r = a.ep_ret[n] + reward;  // episode_rewards += current_reward (:739)
+      const double r = ret0[lane] + reward;  // episode_rewards += current_reward (:739)
       if (terminal && a.final_ret) a.final_ret[n] = r;
       a.ep_ret[n] = autoreset ? 0.0 : r;
     }
@@ -167,6 +174,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
     sc_observe_tail(c, a.t, sink);                                               // (:786)
   }
   __syncthreads();
+  NSTAMP(7);
 
   // out: the tile is this step's observation — obs, or the terminal observation when the
   // env resets now (then wave 0 writes the reset observation to obs), or both
@@ -179,20 +187,26 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
     if (dst0) dst0[n0 * c.O + q] = x;
     if (dst1) dst1[n0 * c.O + q] = x;
   }
-  if (autoreset && w == 0 && live) {  // after the barrier: every wave's heap copy-back landed
-    g.episode = a.episode + 1;
-    sc_reset_env(c, g);
-    ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
-    sc_observe(c, g, 0, out);
+  if (autoreset) {  // after the barrier every wave's heap copy-back has landed
+    if (w == 0 && live) {
+      g.episode = a.episode + 1;
+      sc_reset_env(c, g);  // heaps in HBM, stocks in the LDS copy
+      ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
+      sc_observe(c, g, 0, out);
+    }
+    __syncthreads();
   }
-  if (live && g.overflow) atomicOr(a.err, 1);
+  if (live) {  // the stocks back, one 64-env row per instruction
+    for (int hp = w; hp < NP; hp += W) a.stock[hp * a.n + n] = stk[hp * 64 + lane];
+    if (g.overflow) atomicOr(a.err, 1);
+  }
   NSTAMP(4);
 }
 
 // LDS bytes of one block (the layout above); obs_bytes 4 (float) or 8 (double).
 size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W, int A, int O, int obs_bytes) {
   const size_t NP = static_cast<size_t>(n_nodes) * P;
-  return 64 * ((NP * H + NP + E + n_nodes) * 8 + static_cast<size_t>(O | 1) * obs_bytes +
+  return 64 * ((NP * H + 2 * NP + E + n_nodes + 1) * 8 + static_cast<size_t>(O | 1) * obs_bytes +
                (NP * H + NP + E + n_nodes + W) * 4 + static_cast<size_t>(A | 1) * 4);
 }
 

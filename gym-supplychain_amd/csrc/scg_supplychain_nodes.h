@@ -100,10 +100,19 @@ __host__ __device__ inline bool sc_recv_scan(const HeapView& h, int32_t sz, int 
 __host__ __device__ inline bool sc_nodes_stage(const ScCtx& c, const ScEnv& g, const HeapView& lh, int32_t& lsz,
                                                int t, int i, int p, double& recv) {
   const HeapView gh = sc_heap(c, g, i, p);
-  const int32_t sz = sc_size(c, g, i, p);
   constexpr int kChunk = 4;
-  for (int j0 = 0; j0 < sz; j0 += kChunk) {
-    HeapEntry b[kChunk];
+  // the first chunk is requested with the size (one memory round instead of two for a heap
+  // of at most kChunk entries; slots past the size are read but not used)
+  HeapEntry b[kChunk];
+  const int first = c.H < kChunk ? c.H : kChunk;
+#pragma unroll
+  for (int u = 0; u < kChunk; ++u)
+    if (u < first) b[u] = gh.get(u);
+  const int32_t sz = sc_size(c, g, i, p);
+#pragma unroll
+  for (int u = 0; u < kChunk; ++u)
+    if (u < sz) lh.put(u, b[u]);
+  for (int j0 = kChunk; j0 < sz; j0 += kChunk) {
 #pragma unroll
     for (int u = 0; u < kChunk; ++u)
       if (j0 + u < sz) b[u] = gh.get(j0 + u);

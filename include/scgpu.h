@@ -167,9 +167,11 @@ enum scg_bg_slab_field {
 };
 
 /*
- * STREAM copy of `bytes` (a multiple of 16, 16-byte aligned DEVICE buffers) with `blocks`
- * workgroups of 256 lanes: the achievable-HBM-bandwidth probe bench.py reports beside the
- * 8 TB/s spec (roofline.measured_peak). Not part of the env path.
+ * STREAM copy of `bytes` (a multiple of 16, 16-byte aligned DEVICE buffers): the
+ * achievable-HBM-bandwidth probe bench.py reports beside the 8 TB/s spec
+ * (roofline.measured_peak). blocks == 0: one 16-byte vector per lane, the grid covering the
+ * buffer (the fastest shape measured); blocks > 0: a grid-stride loop over that many
+ * workgroups of 256 lanes. Not part of the env path.
  */
 SCG_API int scg_stream_copy(const void* src, void* dst, int64_t bytes, int32_t blocks, void* stream);
 

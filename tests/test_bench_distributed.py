@@ -2,7 +2,10 @@
 barrier-bracketed timed region with the all_reduce-MAX aggregation, and the end-of-episode
 return all-gather across real auto-reset episode ends — with a CPU stand-in for the GPU
 batch env (oracle.beergame.BeerGameOracle per env, the device's Philox demand per global
-id). Rank 0's gathered returns must equal a 1-rank run over the concatenated shards."""
+id). Rank 0's gathered returns must equal a 1-rank run over the concatenated shards. The
+last test runs bench.run() itself — the whole flow the driver's 8-GPU launch takes: warm-up,
+dry region, headline region, 100 stamped episodes, isolated launches, max over ranks and
+rank 0's JSON line — on two gloo ranks with that stand-in as the platform."""
 import os
 import socket
 
@@ -108,3 +111,114 @@ def test_bench_rank_logic_matches_one_rank_over_concatenated_shards():
     assert one["elapsed_max"] == one["elapsed"] and one["gathers"] == 3
     # the returns are the episode sums of the oracle: the last gathered episode is episode 2
     assert len(one["returns"]) == N_PER_RANK * WORLD and all(isinstance(x, int) for x in one["returns"])
+
+
+# ---- bench.run(), the whole multi-rank flow -----------------------------------------------
+class _Stamp:
+    t = None
+
+
+class CpuPlatform:
+    """bench.Platform for CPU ranks: the stand-in batch env, gloo collectives, wall-clock
+    events stamped by the stand-in's step."""
+
+    def __init__(self, world, rank):
+        import bench
+        self.world, self.rank, self.device = world, rank, "cpu"
+        self._base = bench.Platform()
+
+    def make_env(self, n_envs, env_offset):
+        env = StampedBatch(n_envs, env_offset)
+        return env
+
+    def week_actions(self, env, n_envs):
+        return _week_actions(n_envs, env.env_offset)
+
+    def sync(self):
+        pass
+
+    def barrier(self):
+        dist.barrier()
+
+    def new_event(self):
+        return _Stamp()
+
+    def elapsed_ms(self, a, b):
+        return (b.t - a.t) * 1e3
+
+    def destroy_event(self, ev):
+        pass
+
+    def extras(self):
+        raise AssertionError("extras run on 1-rank jobs only")
+
+    def cpu_baseline(self, budget):
+        raise AssertionError("the CPU baseline runs on 1-rank jobs only")
+
+
+class StampedBatch(CpuBeerGameBatch):
+    """The stand-in with what bench.run() reads: the week plan, error check, stamps."""
+
+    def __init__(self, n, env_offset):
+        super().__init__(n, env_offset)
+        from test_abi import _expected_plan
+        self._plan = _expected_plan([2] * 36, 35)
+
+    def step(self, actions, stamps=None):
+        import time
+        if stamps and stamps[0] is not None:
+            stamps[0].t = time.perf_counter()
+        out = super().step(actions)
+        if stamps and stamps[1] is not None:
+            stamps[1].t = time.perf_counter()
+        return out
+
+    def check_errors(self):
+        pass
+
+
+def _run_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        args = bench.parse_args(["--gpus", str(world), "--envs", "2", "--steps", "20", "--warmup", "5",
+                                 "--kernel-samples", "35", "--no-extras", "--no-cpu-baseline"])
+        line = bench.run(args, CpuPlatform(world, rank))
+        q.put((rank, line))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_run_on_two_ranks_emits_the_rank0_line():
+    import json
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None                                   # only rank 0 prints
+    line = json.loads(json.dumps(res[0]))                   # the line is plain JSON
+    assert line["metric"] == "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X"
+    assert line["n_gpus"] == 2 and line["steps"] == 20 and line["warmup"] == 5
+    assert line["scaling"] == "weak" and line["higher_is_better"] is True and line["unit"] == "env-steps/s"
+    cfg = line["config"]
+    assert cfg["episode_return_allgather"] is True and cfg["parallelism"] == "env-shard x2"
+    assert cfg["n_envs_per_gpu"] == 2
+    # whole-job throughput: envs of both ranks x K over the max-over-ranks wall time
+    assert abs(line["value"] - 2 * 2 * 20 / (line["ms_per_step"] * 20 / 1e3)) < 1e-6 * line["value"]
+    assert line["warmup_steps_run"] == 35 + 20                # one whole episode, then the dry region
+    ep = line["episodes_timed"]
+    assert ep["episodes"] == 100 and ep["steps"] == 3500
+    roof = line["roofline"]
+    assert roof["launches_timed"] == 3500 and roof["isolated_launches"] == 35
+    assert roof["bytes_per_launch"] > 0 and "measured_peak" not in roof and "cpu_baseline" not in line
+    # every episode end of the run was all-gathered: warm-up 35 + dry 20 + headline 20 +
+    # the walk to the boundary + 3,500 + 35 isolated steps
+    total = 35 + 20 + 20 + (35 - (35 + 20 + 20) % 35) % 35 + 3500 + 35
+    assert line["episode_returns_gathered"] == total // 35

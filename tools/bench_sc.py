@@ -85,7 +85,9 @@ def pmc_traffic(symbol, n_envs, name):
     import glob
     if n_envs != SCENARIOS[name]["n_envs"]:
         return None, None
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
+    from bench import profile_tag_key
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), key=profile_tag_key,
+                       reverse=True):
         with open(path) as f:
             traffic = json.load(f).get("traffic", {})
         for k, t in traffic.items():

@@ -4,8 +4,8 @@
     SCG_PKG_ROOT=exp/nstamps python tools/nodes_stamps.py [--envs 65536] [--steps 3]
 
 Runs sc-2perstage-v0 steps with kernel="nodes"; after each, reads the shader-clock stamps
-lane 0 of every wave wrote (scg_sc_nodes.hip NSTAMP: 0 start, 5 heaps staged, 1 acted,
-2 past the barrier, 3 heaps done, 4 end) and prints per phase the median / p90 over waves, split by
+lane 0 of every wave wrote (scg_sc_nodes.hip NSTAMP: 0 start, 5 heaps staged, 6 past the
+first barrier, 1 acted, 2 past the second, 3 heaps done, 7 past the third, 4 end) and prints per phase the median / p90 over waves, split by
 wave index in the block (wave w runs node w), and the spread of wave starts and ends
 (shader clocks, relative to the earliest start).
 """
@@ -49,13 +49,13 @@ def main():
         assert fn(buf.ctypes.data, buf.shape[0]) == 0
         st = buf.astype(np.int64)
         t0 = st[:, 0].min()
-        rel = st[:, :6] - t0
+        rel = st[:, :8] - t0
         out = {"step": s, "waves": int(len(st)), "span": int(rel[:, 4].max()),
                "start_p50_p90_max": [int(np.percentile(rel[:, 0], q)) for q in (50, 90, 100)],
                "end_p10_p50_max": [int(np.percentile(rel[:, 4], q)) for q in (10, 50, 100)]}
-        names = ["stage", "act", "barrier", "heaps", "reward/end", "whole"]
-        d = np.stack([rel[:, 5] - rel[:, 0], rel[:, 1] - rel[:, 5], rel[:, 2] - rel[:, 1], rel[:, 3] - rel[:, 2],
-                      rel[:, 4] - rel[:, 3], rel[:, 4] - rel[:, 0]], 1)
+        names = ["stage", "barrier0", "act", "barrier1", "heaps", "reward+barrier2", "out", "whole"]
+        d = np.stack([rel[:, 5] - rel[:, 0], rel[:, 6] - rel[:, 5], rel[:, 1] - rel[:, 6], rel[:, 2] - rel[:, 1],
+                      rel[:, 3] - rel[:, 2], rel[:, 7] - rel[:, 3], rel[:, 4] - rel[:, 7], rel[:, 4] - rel[:, 0]], 1)
         out["phase_p50_p90"] = {n: [int(np.percentile(d[:, k], 50)), int(np.percentile(d[:, k], 90))]
                                 for k, n in enumerate(names)}
         wi = np.arange(len(st)) % W
