@@ -87,11 +87,20 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   int32_t* ibtk = hsz + NP * 64;
   int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
   int32_t* amb = cost_k + NN * 64;
-  float* act_t = reinterpret_cast<float*>(amb + W * 64);
+  uint32_t* lmask = reinterpret_cast<uint32_t*>(amb + W * 64);  // ledger entry marks [NP][64]
+  float* act_t = reinterpret_cast<float*>(lmask + NP * 64);
   // heaps and sizes in HBM (the batch's base pointers, column n); stocks in the LDS copy
   ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
   g.soff = lane;
   g.hoff = n;
+  const bool ledgers = a.led_v && a.ledp_v;
+  if (ledgers) {  // the nodes' entries to their slots (column n = base + n0 + soff), reduced below
+    g.led_v = a.ledp_v + n0;
+    g.led_k = a.ledp_k + n0;
+    g.led_stride = a.n;
+    g.led_mask = lmask + lane;
+    g.led_mask_stride = 64;
+  }
   auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
   NSTAMP(0);
 
@@ -176,6 +185,26 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   __syncthreads();
   NSTAMP(7);
 
+  // ledgers: entry q of every env, the nodes' entries added in node order (:750-760); at an
+  // auto-reset the finished episode's ledger is kept and the new one starts at int 0
+  if (ledgers && live)
+    for (int q = w; q < 2 * SCG_SC_LEDGER_KEYS * P; q += W) {
+      const int64_t at = q * a.n + n;
+      double lv = a.led_v[at];
+      int32_t lk = a.led_k[at];
+      sc_ledger_reduce(c, q, a.ledp_v + n, a.ledp_k + n, a.n, lmask + lane, 64, lv, lk);
+      if (autoreset) {
+        if (a.led_fv) {
+          a.led_fv[at] = lv;
+          a.led_fk[at] = lk;
+        }
+        lv = 0.0;
+        lk = np_kind_abi(NK_INT);
+      }
+      a.led_v[at] = lv;
+      a.led_k[at] = lk;
+    }
+
   // out: the tile is this step's observation — obs, or the terminal observation when the
   // env resets now (then wave 0 writes the reset observation to obs), or both
   ObsT* const dst0 = static_cast<ObsT*>(autoreset ? a.term_obs : a.obs);
@@ -190,6 +219,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   if (autoreset) {  // after the barrier every wave's heap copy-back has landed
     if (w == 0 && live) {
       g.episode = a.episode + 1;
+      g.led_v = nullptr;   // the ledger was restarted above
       sc_reset_env(c, g);  // heaps in HBM, stocks in the LDS copy
       ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
       sc_observe(c, g, 0, out);
@@ -207,7 +237,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
 size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W, int A, int O, int obs_bytes) {
   const size_t NP = static_cast<size_t>(n_nodes) * P;
   return 64 * ((NP * H + 2 * NP + E + n_nodes + 1) * 8 + static_cast<size_t>(O | 1) * obs_bytes +
-               (NP * H + NP + E + n_nodes + W) * 4 + static_cast<size_t>(A | 1) * 4);
+               (NP * H + 2 * NP + E + n_nodes + W) * 4 + static_cast<size_t>(A | 1) * 4);
 }
 
 // Widest destination list the kernel is instantiated for (its split runs in registers).

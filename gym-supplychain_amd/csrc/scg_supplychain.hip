@@ -204,8 +204,15 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
 // is staged in LDS ([slot][lane], lane fastest: conflict free), the
 // shipments go through the env's HBM inbox, the node's observation is written while its
 // heaps are staged. No block-wide barrier: every lane only touches its own LDS column.
+#ifndef SCG_STAGED_WPE
+#define SCG_STAGED_WPE 0  // 0: the compiler's choice
+#endif
 template <int MAXD>
-__global__ __launch_bounds__(kScBlock) void sc_step_staged_kernel(const ScArgs a) {
+__global__ __launch_bounds__(kScBlock)
+#if SCG_STAGED_WPE
+__attribute__((amdgpu_waves_per_eu(SCG_STAGED_WPE)))
+#endif
+void sc_step_staged_kernel(const ScArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x;
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + lane;
@@ -397,7 +404,8 @@ int sc_check(const scg_sc_config* cfg, const scg_sc_state* st) {
     return fail(SCG_ERR_INVALID, "global env ids must fit in 32 bits");
   if (!st->stock || !st->heap_tk || !st->heap_val || !st->heap_size || !st->error_flags)
     return fail(SCG_ERR_INVALID, "state buffers stock/heap_tk/heap_val/heap_size/error_flags are required");
-  if (!st->ledger != !st->ledger_kind || !st->final_ledger != !st->final_ledger_kind)
+  if (!st->ledger != !st->ledger_kind || !st->final_ledger != !st->final_ledger_kind ||
+      !st->ledger_part != !st->ledger_part_kind)
     return fail(SCG_ERR_INVALID, "ledger values and kinds come in pairs");
   if (st->ledger && cfg->kernel == SCG_SC_KERNEL_LEVEL)
     return fail(SCG_ERR_INVALID, "build_info ledgers need the lane kernel");
@@ -444,6 +452,8 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   a.led_k = st->ledger_kind;
   a.led_fv = st->final_ledger;
   a.led_fk = st->final_ledger_kind;
+  a.ledp_v = st->ledger_part;
+  a.ledp_k = st->ledger_part_kind;
   a.n = st->n_envs;
   a.env_offset = st->env_offset;
   a.episode = st->episode;
@@ -784,7 +794,7 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
       default: SCG_LEVEL_LAUNCH(32); break;
     }
 #undef SCG_LEVEL_LAUNCH
-  } else if (cfg->kernel == SCG_SC_KERNEL_NODES && !st->ledger) {
+  } else if (cfg->kernel == SCG_SC_KERNEL_NODES && (!st->ledger || st->ledger_part)) {
     if (cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST || cfg->inbox_size < 0)
       return fail(SCG_ERR_INVALID, "node-parallel kernel needs the layout and inbox scg_sc_prepare derives");
     if (int rc = sc_launch_nodes(a, sc_maxd_bucket(cfg->max_dests), cfg->group, cfg->inbox_size, s)) return rc;

@@ -99,6 +99,14 @@ struct ScEnv {
   // them wave-uniform (SGPRs) instead of one 64-bit VGPR pair per pointer and lane.
   int64_t soff = 0;
   int64_t hoff = 0;
+  // Ledger entries by node (node-parallel kernel, where the nodes act at once): with led_mask
+  // set, sc_note stores node led_node's entry in its own slot ((node * 2 + part) * 8 + key) *
+  // P + p of led_v/led_k and marks it in the node's per-product word led_mask[(node * P + p) *
+  // led_mask_stride] (bit part * 8 + key); sc_ledger_reduce adds the marked slots to the
+  // ledger in node order afterwards, as _update_statistics does (:750-760).
+  int32_t led_node = 0;
+  uint32_t* led_mask = nullptr;
+  int64_t led_mask_stride = 0;
 };
 
 // info['sc_episode'] categories in the reference's dict order (:416-417)
@@ -113,6 +121,16 @@ enum ScLedgerKey : int {
 // change neither value nor type of a sum, so they are skipped.
 __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int key, int p, Num cost, Num units) {
   if (!e.led_v) return;
+  if (e.led_mask) {  // by node: the slot of this node's entry, reduced in node order later
+    const int64_t s0 = ((static_cast<int64_t>(e.led_node) * 2 * SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride + e.soff;
+    const int64_t s1 = s0 + static_cast<int64_t>(SCG_SC_LEDGER_KEYS) * c.P * e.led_stride;
+    e.led_v[s0] = cost.v;
+    e.led_k[s0] = np_kind_abi(cost.k);
+    e.led_v[s1] = units.v;
+    e.led_k[s1] = np_kind_abi(units.k);
+    e.led_mask[(static_cast<int64_t>(e.led_node) * c.P + p) * e.led_mask_stride] |= (1u << key) | (1u << (8 + key));
+    return;
+  }
   const int64_t i0 = (static_cast<int64_t>(key) * c.P + p) * e.led_stride + e.soff;
   const int64_t i1 = (static_cast<int64_t>(SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride + e.soff;
   const Num a = np_add(Num{e.led_v[i0], np_kind_int(e.led_k[i0])}, cost);
@@ -121,6 +139,31 @@ __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int k
   e.led_k[i0] = np_kind_abi(a.k);
   e.led_v[i1] = b.v;
   e.led_k[i1] = np_kind_abi(b.k);
+}
+
+// A node is about to act (node-parallel kernel with ledgers): its entries go to its slots.
+__host__ __device__ __forceinline__ void sc_led_begin_node(const ScCtx& c, ScEnv& e, int node) {
+  if (!e.led_v || !e.led_mask) return;
+  e.led_node = node;
+  for (int p = 0; p < c.P; ++p) e.led_mask[(static_cast<int64_t>(node) * c.P + p) * e.led_mask_stride] = 0;
+}
+
+// Ledger entry q = (part * 8 + key) * P + p of one env after the step: the nodes' marked
+// entries added in node order (:750-760) to (lv, lk). cv/ck: the slots (stride cstride);
+// mask: the per-(node, product) words (stride mstride).
+__host__ __device__ inline void sc_ledger_reduce(const ScCtx& c, int q, const double* cv, const int32_t* ck,
+                                                 int64_t cstride, const uint32_t* mask, int64_t mstride, double& lv,
+                                                 int32_t& lk) {
+  const int p = q % c.P, pk = q / c.P;  // pk = part * 8 + key
+  const uint32_t bit = 1u << pk;
+  Num acc{lv, np_kind_int(lk)};
+  for (int i = 0; i < c.n_nodes; ++i) {
+    if (!(mask[(static_cast<int64_t>(i) * c.P + p) * mstride] & bit)) continue;
+    const int64_t s = ((static_cast<int64_t>(i) * 2 * SCG_SC_LEDGER_KEYS + pk) * c.P + p) * cstride;
+    acc = np_add(acc, Num{cv[s], np_kind_int(ck[s])});
+  }
+  lv = acc.v;
+  lk = np_kind_abi(acc.k);
 }
 
 // est_episode at reset (:684-695): every entry the Python int 0

@@ -134,6 +134,7 @@ __host__ __device__ inline Num sc_nodes_act(const ScCtx& c, ScEnv& g, const Node
     st = st + recv[p * rstride];  // self.stock += arrived_material (:228)
   }
   if (!c.nodes[i].last_level) in.clear(c, i);
+  sc_led_begin_node(c, g, i);
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   return sc_node_act<MAXD, NodesInbox, true>(c, g, ltc, dmc, i, act, t, in);
 }
@@ -192,6 +193,7 @@ __host__ __device__ inline double sc_nodes_serial(const ScCtx& c, ScEnv& g, cons
       sc_nodes_heap(c, g, heap_at(hp), sz[hp * sz_stride], in, ltc, act, t, i, p, a_i, lt_i, out, true);
     }
     if (!c.nodes[i].last_level) in.clear(c, i);
+    sc_led_begin_node(c, g, i);
     total = np_add(total, sc_node_act<MAXD, NodesInbox, true>(c, g, ltc, dmc, i, act, t, in));
     for (int p = 0; p < c.P; ++p) sc_observe_stock(c, g, i, p, out);
   }

@@ -227,7 +227,8 @@ class SupplyChainVecEnv:
     {key: [N, P]}, 'units': {key: [N, P]}} (device views, float64; the NumPy type of every
     entry in ledger_kinds()), the reference's episode ledgers (:684-695, :750-760); with
     auto-reset the terminal step adds 'terminal_sc_episode' for the finished episode.
-    Lane and staged kernels.
+    Every kernel but the level kernel (the node-parallel one keeps each node's entries of a
+    step apart and adds them in node order, :750-760).
     """
 
     _KERNELS = {"auto": nat.SC_KERNEL_AUTO, "lane": nat.SC_KERNEL_LANE, "level": nat.SC_KERNEL_LEVEL,
@@ -276,7 +277,8 @@ class SupplyChainVecEnv:
             raise ValueError(f"kernel must be one of {sorted(self._KERNELS)}, got {kernel!r}")
         c.kernel = self._KERNELS[kernel]
         if spec.build_info and c.kernel == nat.SC_KERNEL_LEVEL:
-            raise ValueError("build_info ledgers are kept by the lane and staged kernels (kernel='lane', 'staged' or 'auto')")
+            raise ValueError("build_info ledgers are kept by the lane, staged and node-parallel kernels "
+                             "(kernel='lane', 'staged', 'nodes' or 'auto')")
         nat.check(nat.lib.scg_sc_prepare(ctypes.byref(c), host_nodes))
         self.kernel = {nat.SC_KERNEL_LEVEL: "level", nat.SC_KERNEL_STAGED: "staged",
                        nat.SC_KERNEL_NODES: "nodes"}.get(c.kernel, "lane")
@@ -354,6 +356,11 @@ class SupplyChainVecEnv:
                 self._fled = torch.zeros(shape, dtype=torch.float64, device=dev)
                 self._fled_k = torch.zeros(shape, dtype=torch.int32, device=dev)
                 s.final_ledger, s.final_ledger_kind = self._fled.data_ptr(), self._fled_k.data_ptr()
+            if self.kernel == "nodes":  # each node's entries of a step [NN * 2 * 8 * P][N]
+                pshape = (NN * 2 * nat.SC_LEDGER_KEYS * P, n_envs)
+                self._led_part = torch.zeros(pshape, dtype=torch.float64, device=dev)
+                self._led_part_k = torch.zeros(pshape, dtype=torch.int32, device=dev)
+                s.ledger_part, s.ledger_part_kind = self._led_part.data_ptr(), self._led_part_k.data_ptr()
             if not track_returns:
                 raise ValueError("build_info needs track_returns (sc_episode['rewards'])")
         self._st = s
@@ -462,8 +469,8 @@ class SupplyChainVecEnv:
             return f"scg::sc_level_kernel<{maxd}, {'true' if c.level_staged else 'false'}>"
         if self.kernel == "staged":
             return f"scg::sc_step_staged_kernel<{maxd}>"
-        if self.kernel == "nodes" and not self.spec.build_info:
-            return f"scg::sc_step_nodes_kernel<{maxd}>"
+        if self.kernel == "nodes":
+            return f"scg::sc_step_nodes_kernel<{maxd}, {'true' if c.obs_f64 else 'false'}>"
         lds = 64 * len(self.spec.nodes) * self.spec.P * (12 * c.heap_capacity + 4)
         if lds > 64 * 1024:
             return f"scg::sc_step_kernel<{maxd}>"

@@ -393,7 +393,8 @@ typedef struct scg_sc_state {
   int32_t* error_flags;         /* [1] DEVICE, sticky: bit 0 = a heap exceeded capacity    */
   int32_t* inbox_tk;            /* [inbox_size][N] staged kernel: shipment time<<3|kind, -1 = none */
   double* inbox_val;            /* [inbox_size][N] staged kernel: shipment amount               */
-  /* build_info ledgers, info['sc_episode'] (:684-695, :750-760): optional, lane kernel only.
+  /* build_info ledgers, info['sc_episode'] (:684-695, :750-760): optional (every kernel but
+     the level kernel).
      Entry ((part * SCG_SC_LEDGER_KEYS + key) * P + p), part 0 = costs, 1 = units, keys in
      the reference's order (stock, stock_pen, supply, process, process_pen, ship, ship_pen,
      unmet_dem); value in ledger, NumPy type (0 int, 1 float, 2 float32, 3 float64, 4 int64)
@@ -402,6 +403,12 @@ typedef struct scg_sc_state {
   int32_t* ledger_kind;         /* [2 * 8 * P][N] */
   double* final_ledger;         /* [2 * 8 * P][N] optional */
   int32_t* final_ledger_kind;   /* [2 * 8 * P][N] optional */
+  /* Node-parallel kernel with ledgers: each node's entries of the step, [n_nodes * 2 * 8 * P][N]
+   * (slot ((node * 2 + part) * 8 + key) * P + p), added to the ledger in node order after the
+   * step (:750-760). Without them a ledger step of a SCG_SC_KERNEL_NODES config runs the lane
+   * kernel on the same state. */
+  double* ledger_part;
+  int32_t* ledger_part_kind;
 } scg_sc_state;
 
 /* sizeof(scg_sc_node), sizeof(scg_sc_config), sizeof(scg_sc_state), to check FFI bindings. */

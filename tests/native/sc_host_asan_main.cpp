@@ -6,7 +6,7 @@
 //   sc_host_asan JOBS OUT
 // JOBS holds a sequence of jobs, each one episode of one env in one kernel body (mode: 0
 // lane, 1 level, 2 staged, 3 node-parallel phases with the nodes in reverse order, 4 the
-// node-parallel serial walk, 5 lane with build_info ledgers); OUT receives, per job, the
+// node-parallel serial walk, 5 lane; ledgers kept from mode 2 on); OUT receives, per job, the
 // return code and every snapshot the shared library's sch_episode_* entry points return.
 // Layout of a job (little endian): int32 magic 0x53434A42, mode, cfg_bytes, node_bytes,
 // n_nodes, thr_len, dthr_len, dbase_len, steps, A, O, NP, H, P; uint64 seed; uint32 env_id,
@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
         val(static_cast<size_t>(steps + 1) * NP * H), led_v(static_cast<size_t>(steps) * 2 * 8 * P);
     std::vector<int32_t> tk(static_cast<size_t>(steps + 1) * NP * H), sz(static_cast<size_t>(steps + 1) * NP),
         led_k(led_v.size());
-    const bool ledger = mode == 2 || mode == 5;
+    const bool ledger = mode >= 2;  // staged, node-parallel (by-node slots) and lane kernels
     const int impl = mode == 5 ? 0 : mode;
     const int32_t rc = episode_impl(impl, &cfg, nodes.data(), thr.data(), seed, ids[0], ids[1], steps, acts.data(),
                                     obs.data(), rew.data(), stock.data(), tk.data(), val.data(), sz.data(),

@@ -119,6 +119,23 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
     }
     if (mode == 3 || mode == 4) {  // sc_step_nodes_kernel's phases (4: its serial walk every step); nodes in REVERSE order (they are independent)
       const int E = cfg->inbox_size > 0 ? cfg->inbox_size : 1;
+      // ledgers by node, reduced in node order after the step (the kernel's ledger phase)
+      std::vector<double> part_v(static_cast<size_t>(c.n_nodes) * LQ, -7.0);
+      std::vector<int32_t> part_k(part_v.size(), 99);
+      std::vector<uint32_t> marks(NP, 0xdeadbeefu);
+      if (ledger) {
+        et.led_v = part_v.data();
+        et.led_k = part_k.data();
+        et.led_stride = 1;
+        et.led_mask = marks.data();
+        et.led_mask_stride = 1;
+      }
+      auto reduce_ledger = [&]() {
+        if (!ledger) return;
+        for (int q = 0; q < LQ; ++q) scg::sc_ledger_reduce(c, q, part_v.data(), part_k.data(), 1, marks.data(), 1, led_v[q], led_k[q]);
+        std::memcpy(ledger + static_cast<int64_t>(t - 1) * LQ, led_v.data(), sizeof(double) * LQ);
+        std::memcpy(ledger_kind + static_cast<int64_t>(t - 1) * LQ, led_k.data(), sizeof(int32_t) * LQ);
+      };
       std::vector<int32_t> htk(static_cast<size_t>(NP) * c.H, 0x7fffffff), hsz(NP, -1), ibtk(E, 0x7fffffff);
       std::vector<double> hval(htk.size(), -1.0), recv(NP, -1.0), ibval(E, -1.0);
       std::vector<scg::Num> cost(c.n_nodes);
@@ -143,6 +160,7 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
         rewards[t - 1] = r;
         for (int k = 0; k < c.R * c.P; ++k) scg::sc_observe_demand(c, et, t, k, out);
         scg::sc_observe_tail(c, t, out);
+        reduce_ledger();
         if (et.overflow) return 1;
         continue;
       }
@@ -167,6 +185,7 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
       rewards[t - 1] = scg::np_neg(total).v;
       for (int k = 0; k < c.R * c.P; ++k) scg::sc_observe_demand(c, et, t, k, out);
       scg::sc_observe_tail(c, t, out);
+      reduce_ledger();
       if (et.overflow) return 1;
       continue;
     }
@@ -250,6 +269,15 @@ extern "C" int sch_episode_nodes(const scg_sc_config* cfg, const scg_sc_node* no
                                  int32_t* heap_size) {
   return episode_impl(3, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock, heap_tk,
                       heap_val, heap_size);
+}
+
+extern "C" int sch_episode_nodes_ledger(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,
+                                        uint64_t seed, uint32_t env_id, uint32_t episode, int32_t steps,
+                                        const float* actions, double* obs, double* rewards, double* stock,
+                                        int32_t* heap_tk, double* heap_val, int32_t* heap_size, double* ledger,
+                                        int32_t* ledger_kind, int32_t serial) {
+  return episode_impl(serial ? 4 : 3, cfg, nodes, lt_thr, seed, env_id, episode, steps, actions, obs, rewards, stock,
+                      heap_tk, heap_val, heap_size, ledger, ledger_kind);
 }
 
 extern "C" int sch_episode_nodes_serial(const scg_sc_config* cfg, const scg_sc_node* nodes, const uint32_t* lt_thr,

@@ -29,6 +29,7 @@ def build():
     lib.sch_episode_nodes.restype = ctypes.c_int
     lib.sch_nodes_fallbacks.restype = ctypes.c_int
     lib.sch_episode_nodes_serial.restype = ctypes.c_int
+    lib.sch_episode_nodes_ledger.restype = ctypes.c_int
     return lib
 
 
@@ -54,6 +55,9 @@ def run_episode(lib, cfg, nodes, lt_thr, seed, env_id, episode, actions, level=F
     if ledger or staged:
         led_v = np.zeros((T, 2, 8, cfg.n_products))
         led_k = np.zeros((T, 2, 8, cfg.n_products), dtype=np.int32)
+        if nodes_kernel:  # the node-parallel phases with ledgers kept by node, reduced in node order
+            rc = lib.sch_episode_nodes_ledger(*args, p(led_v), p(led_k), ctypes.c_int32(int(nodes_serial)))
+            return rc, obs, rew, stock, (tk, val, size), (led_v, led_k)
         fn = lib.sch_episode_staged if staged else lib.sch_episode_ledger
         rc = fn(*args, p(led_v), p(led_k))
         return rc, obs, rew, stock, (tk, val, size), (led_v, led_k)

@@ -274,17 +274,18 @@ def test_level_kernel_equals_lane_kernel(scenario, kw):
         e.check_errors()
 
 
-@pytest.mark.parametrize("kernel", ["lane", "staged"])
+@pytest.mark.parametrize("kernel", ["lane", "staged", "nodes"])
 @pytest.mark.parametrize("name", CASES)
 def test_ledgers_match_reference(name, kernel):
     """build_info: info['sc_episode'] on the device against the reference's ledgers after
-    every step — values and NumPy types of every cost/unit entry, exactly (both kernels
-    that keep ledgers)."""
+    every step — values and NumPy types of every cost/unit entry, exactly (every kernel
+    that keeps ledgers; the node-parallel one where its LDS takes the chain)."""
     from gym_supplychain_amd import _native as nat
     g = load_sc(name)
     meta = g["meta"]
     T, N = meta["T"], g["obs"].shape[1]
-    env = _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, build_info=True, kernel=kernel)
+    env = _or_skip(lambda: _vec(meta, N, obs_dtype=torch.float64, auto_reset=False, build_info=True, kernel=kernel),
+                   kernel)
     assert env.kernel == kernel
     env.reset()
     acts = torch.as_tensor(g["actions"], device=DEV)
@@ -377,7 +378,9 @@ def test_auto_kernel_symbols():
     node-staged kernel (config 4); kernel_symbol names what rocprofv3 reports."""
     import gym_supplychain_amd as gsa
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV)
-    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2>"
+    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2, false>"
+    env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, build_info=True)
+    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2, false>"
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, kernel="lane")
     assert env.kernel == "lane" and env.kernel_symbol == "scg::sc_step_lds_kernel<2, 32>"
     cus = torch.cuda.get_device_properties(DEV).multi_processor_count

@@ -164,6 +164,29 @@ def test_host_build_of_node_parallel_kernel_matches_reference(harness, name, ser
     assert harness.sch_nodes_fallbacks() == 0, name
 
 
+@pytest.mark.parametrize("serial", [False, True])
+@pytest.mark.parametrize("name", CASES)
+def test_host_build_of_node_parallel_ledgers_match_reference(harness, name, serial):
+    """build_info in the node-parallel kernel: each node's act stores its entries in slots of
+    its own (the nodes act at once, in reverse order here), and the step's ledger adds them
+    in node order afterwards (sc_ledger_reduce, :750-760) — values and NumPy types of every
+    entry against the reference after every step, exactly."""
+    import native_harness
+    from gym_supplychain_amd import _native as nat
+    g = load_sc(name)
+    meta = g["meta"]
+    spec, c, nodes, thr = _setup(g, nat.SC_KERNEL_STAGED)
+    for n in range(g["obs"].shape[1]):
+        rc, obs, rew, _, _, (led_v, led_k) = native_harness.run_episode(
+            harness, c, nodes, thr, meta["seed"], n, 0, g["actions"][:, n], ledger=True, nodes_kernel=True,
+            nodes_serial=serial)
+        assert rc == 0
+        assert np.array_equal(obs, g["obs"][:, n]), name
+        assert np.array_equal(led_v[:, 0], g["led_cost"][:, n]) and np.array_equal(led_v[:, 1], g["led_units"][:, n])
+        assert np.array_equal(led_k[:, 0], g["led_cost_k"][:, n]), name
+        assert np.array_equal(led_k[:, 1], g["led_units_k"][:, n]), name
+
+
 def test_recv_scan_flags_float32_ties():
     """sc_recv_scan's fallback condition: two due amounts NumPy compares as equal (a float32
     against a Python float, compared in float32) with different doubles make the heappop

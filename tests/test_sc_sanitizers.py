@@ -114,7 +114,7 @@ def test_sanitized_kernel_bodies_match_reference(name, tmp_path):
                 k = int(r["size"][s_, hp])
                 assert (r["tk"][s_, hp, :k] >> 3).tolist() == gt[s_, hp, :k].tolist(), (name, m, n, s_)
                 assert r["val"][s_, hp, :k].tolist() == gv[s_, hp, :k].tolist(), (name, m, n, s_)
-        if m in (2, 5):
+        if m >= 2:
             assert np.array_equal(r["led_v"][:, 0], g["led_cost"][:, n]), (name, m, n)
             assert np.array_equal(r["led_v"][:, 1], g["led_units"][:, n]), (name, m, n)
             assert np.array_equal(r["led_k"][:, 0], g["led_cost_k"][:, n]), (name, m, n)

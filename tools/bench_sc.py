@@ -96,14 +96,14 @@ def pmc_traffic(symbol, n_envs, name):
     return None, None
 
 
-def run(name, steps, warmup, n_envs, cpu, kernel="auto"):
+def run(name, steps, warmup, n_envs, cpu, kernel="auto", build_info=False):
     import torch
     import gym_supplychain_amd as gsa
     sc = SCENARIOS[name]
     N = n_envs or sc["n_envs"]
     dev = torch.device("cuda", 0)
     env = gsa.make_vec(sc["env_id"], N, seed=0, device=dev, obs_dtype=torch.float32, auto_reset=True, kernel=kernel,
-                       **sc["kwargs"])
+                       build_info=build_info, **sc["kwargs"])
     gen = torch.Generator(device=dev).manual_seed(0)
     pool = [torch.rand((N, env.n_actions), generator=gen, device=dev) * 2 - 1 for _ in range(4)]
     env.reset()
@@ -131,7 +131,8 @@ def run(name, steps, warmup, n_envs, cpu, kernel="auto"):
             "data": "synthetic: uniform demand drawn on device (Philox4x32-10), U[-1,1] float32 actions",
             "config": {"workload": f"{sc['env_id']} step() (BASELINE {sc['baseline_cfg']})", "n_envs": N,
                        "kernel": env.kernel,
-                       "n_actions": env.n_actions, "n_obs": env.n_obs, "heap_capacity": env.heap_capacity},
+                       "n_actions": env.n_actions, "n_obs": env.n_obs, "heap_capacity": env.heap_capacity,
+                       "build_info": build_info},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": bpe * N, "kernel": env.kernel_symbol,
@@ -151,13 +152,14 @@ def main():
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "staged", "nodes", "all", "both"])
+    ap.add_argument("--build-info", action="store_true", help="keep the build_info ledgers (info['sc_episode'])")
     a = ap.parse_args()
     for name in (["2perstage", "ntom"] if a.scenario == "both" else [a.scenario]):
         kernels = [a.kernel]
         if a.kernel in ("all", "both"):  # the node-parallel kernel only takes chains whose block fits LDS
             kernels = ["lane", "level", "staged"] + (["nodes"] if name == "2perstage" else [])
         for k in kernels:
-            run(name, a.steps, a.warmup, a.envs, not a.no_cpu_baseline and k == kernels[-1], k)
+            run(name, a.steps, a.warmup, a.envs, not a.no_cpu_baseline and k == kernels[-1], k, a.build_info)
 
 
 if __name__ == "__main__":
