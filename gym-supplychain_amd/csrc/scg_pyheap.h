@@ -48,9 +48,12 @@ struct HeapView {
   __host__ __device__ __forceinline__ int32_t time_at(int i) const { return he_time(tk[i * stride]); }
 };
 
-// heapq._siftdown(heap, startpos, pos)
-__host__ __device__ inline void py_siftdown(const HeapView& h, int startpos, int pos) {
-  const HeapEntry item = h.get(pos);
+// heapq._siftdown(heap, startpos, pos) with the moving item (the entry at pos) held in
+// registers: it is written once, at its final position. Every variant below keeps the
+// entries being moved in registers the same way, so each heap slot is read once per sift
+// level (the heap is in LDS in every kernel but the lane one on HBM heaps: these reads are
+// a chain of dependent latencies).
+__host__ __device__ inline void py_siftdown_item(const HeapView& h, int startpos, int pos, const HeapEntry& item) {
   while (pos > startpos) {
     const int parentpos = (pos - 1) >> 1;
     const HeapEntry parent = h.get(parentpos);
@@ -64,28 +67,41 @@ __host__ __device__ inline void py_siftdown(const HeapView& h, int startpos, int
   h.put(pos, item);
 }
 
-// heapq._siftup(heap, pos): move the smaller child up to a leaf, then sift down.
-__host__ __device__ inline void py_siftup(const HeapView& h, int size, int pos) {
+__host__ __device__ inline void py_siftdown(const HeapView& h, int startpos, int pos) {
+  py_siftdown_item(h, startpos, pos, h.get(pos));
+}
+
+// heapq._siftup(heap, pos) for `item` standing at pos: move the smaller child up to a leaf,
+// then sift the item down from there (CPython's bottom-up variant).
+__host__ __device__ inline void py_siftup_item(const HeapView& h, int size, int pos, const HeapEntry& item) {
   const int startpos = pos;
-  const HeapEntry item = h.get(pos);
   int childpos = 2 * pos + 1;
   while (childpos < size) {
     const int rightpos = childpos + 1;
-    if (rightpos < size && !he_less(h.get(childpos), h.get(rightpos))) childpos = rightpos;
-    h.put(pos, h.get(childpos));
+    HeapEntry child = h.get(childpos);
+    if (rightpos < size) {
+      const HeapEntry right = h.get(rightpos);
+      if (!he_less(child, right)) {
+        childpos = rightpos;
+        child = right;
+      }
+    }
+    h.put(pos, child);
     pos = childpos;
     childpos = 2 * pos + 1;
   }
-  h.put(pos, item);
-  py_siftdown(h, startpos, pos);
+  py_siftdown_item(h, startpos, pos, item);
+}
+
+__host__ __device__ inline void py_siftup(const HeapView& h, int size, int pos) {
+  py_siftup_item(h, size, pos, h.get(pos));
 }
 
 // heapq.heappush. Returns false (and pushes nothing) when the heap is full.
 __host__ __device__ inline bool py_heappush(const HeapView& h, int32_t& size, int cap, const HeapEntry& e) {
   if (size >= cap) return false;
-  h.put(size, e);
   ++size;
-  py_siftdown(h, 0, size - 1);
+  py_siftdown_item(h, 0, size - 1, e);  // heap.append(e); _siftdown(heap, 0, len - 1)
   return true;
 }
 
@@ -95,8 +111,7 @@ __host__ __device__ inline HeapEntry py_heappop(const HeapView& h, int32_t& size
   const HeapEntry last = h.get(size);
   if (size > 0) {
     const HeapEntry ret = h.get(0);
-    h.put(0, last);
-    py_siftup(h, size, 0);
+    py_siftup_item(h, size, 0, last);  // heap[0] = last; _siftup(heap, 0)
     return ret;
   }
   return last;

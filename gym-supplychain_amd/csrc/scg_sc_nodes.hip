@@ -57,12 +57,34 @@ namespace scg {
 
 constexpr int kNodesMaxWaves = 8;
 
+// Row and column (r, k) of element q = r * width + k of a row-major tile, walked from q0 in
+// steps of `step` with one division up front (the step's share is wave-uniform).
+struct TileWalk {
+  int r, k, dr, dk, width;
+  __device__ __forceinline__ TileWalk(int q0, int step, int w) : width(w) {
+    r = q0 / w;
+    k = q0 - r * w;
+    dr = step / w;
+    dk = step - dr * w;
+  }
+  __device__ __forceinline__ void next() {
+    r += dr;
+    k += dk;
+    if (k >= width) {
+      k -= width;
+      ++r;
+    }
+  }
+};
+
 #ifndef SCG_NODES_WPE
 #define SCG_NODES_WPE 4
 #endif
 // Four waves per SIMD (<= 128 VGPRs): two blocks of eight waves per CU, which is also what
 // their LDS allows.
-template <int MAXD, bool F64>
+// F64: float64 observations; LED: build_info ledgers (a separate instantiation, so the
+// ledger code costs the common run nothing).
+template <int MAXD, bool F64, bool LED>
 __global__ __launch_bounds__(64 * kNodesMaxWaves) __attribute__((amdgpu_waves_per_eu(SCG_NODES_WPE)))
 void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   using ObsT = typename std::conditional<F64, double, float>::type;
@@ -93,7 +115,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
   g.soff = lane;
   g.hoff = n;
-  const bool ledgers = a.led_v && a.ledp_v;
+  constexpr bool ledgers = LED;
   if (ledgers) {  // the nodes' entries to their slots (column n = base + n0 + soff), reduced below
     g.led_v = a.ledp_v + n0;
     g.led_k = a.ledp_k + n0;
@@ -113,11 +135,8 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   // stage: every heap of the wave's nodes, and the block's action rows into the tile
   {
     const float* src = a.act + n0 * c.A;
-    const int total = nb * c.A;
-    for (int q = threadIdx.x; q < total; q += blockDim.x) {
-      const int r = q / c.A;
-      act_t[r * Ap + (q - r * c.A)] = src[q];
-    }
+    TileWalk tw(threadIdx.x, blockDim.x, c.A);
+    for (int q = threadIdx.x; q < nb * c.A; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
   }
   bool bad = false;
   if (live) {
@@ -209,10 +228,9 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   // env resets now (then wave 0 writes the reset observation to obs), or both
   ObsT* const dst0 = static_cast<ObsT*>(autoreset ? a.term_obs : a.obs);
   ObsT* const dst1 = (terminal && !autoreset) ? static_cast<ObsT*>(a.term_obs) : nullptr;
-  const int cells = nb * c.O;
-  for (int q = threadIdx.x; q < cells; q += blockDim.x) {
-    const int r = q / c.O;
-    const ObsT x = obs_t[r * Op + (q - r * c.O)];
+  TileWalk tw(threadIdx.x, blockDim.x, c.O);
+  for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
+    const ObsT x = obs_t[tw.r * Op + tw.k];
     if (dst0) dst0[n0 * c.O + q] = x;
     if (dst1) dst1[n0 * c.O + q] = x;
   }
@@ -263,7 +281,7 @@ size_t sc_nodes_lds_max() {
   return v;
 }
 
-template <int MAXD, bool F64>
+template <int MAXD, bool F64, bool LED>
 int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
   static std::atomic<bool> raised[64] = {};  // per device
   const size_t lds = sc_nodes_lds_bytes(a.c.n_nodes, a.c.P, a.c.H, E, W, a.c.A, a.c.O, F64 ? 8 : 4);
@@ -271,25 +289,33 @@ int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   if (lds > 64 * 1024 && !raised[dev].load(std::memory_order_acquire)) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sc_step_nodes_kernel<MAXD, F64>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sc_step_nodes_kernel<MAXD, F64, LED>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sc_nodes_lds_max())) != hipSuccess)
       return fail(SCG_ERR_HIP, "node-parallel kernel: cannot raise its LDS limit");
     raised[dev].store(true, std::memory_order_release);
   }
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_nodes_kernel<MAXD, F64>), dim3(static_cast<unsigned>((a.n + 63) / 64)),
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_nodes_kernel<MAXD, F64, LED>), dim3(static_cast<unsigned>((a.n + 63) / 64)),
                      dim3(64 * W), lds, s, a, W, E);
   return check_launch("sc_step_nodes_kernel");
 }
 
 int sc_launch_nodes(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t s) {
   if (W < 1 || W > kNodesMaxWaves) return fail(SCG_ERR_INVALID, "node-parallel kernel: %d waves per block", W);
-  const bool f64 = a.obs_f64 != 0;
+  const int v = (a.obs_f64 ? 1 : 0) | (a.led_v && a.ledp_v ? 2 : 0);
+#define SCG_NODES_CASES(D)                                  \
+  switch (v) {                                              \
+    case 0: return sc_launch_nodes_d<D, false, false>(a, W, E, s); \
+    case 1: return sc_launch_nodes_d<D, true, false>(a, W, E, s);  \
+    case 2: return sc_launch_nodes_d<D, false, true>(a, W, E, s);  \
+    default: return sc_launch_nodes_d<D, true, true>(a, W, E, s);  \
+  }
   switch (maxd_bucket) {
-    case 2: return f64 ? sc_launch_nodes_d<2, true>(a, W, E, s) : sc_launch_nodes_d<2, false>(a, W, E, s);
-    case 4: return f64 ? sc_launch_nodes_d<4, true>(a, W, E, s) : sc_launch_nodes_d<4, false>(a, W, E, s);
-    case 8: return f64 ? sc_launch_nodes_d<8, true>(a, W, E, s) : sc_launch_nodes_d<8, false>(a, W, E, s);
+    case 2: SCG_NODES_CASES(2)
+    case 4: SCG_NODES_CASES(4)
+    case 8: SCG_NODES_CASES(8)
     default: return fail(SCG_ERR_INVALID, "node-parallel kernel: nodes ship to at most 8 destinations");
   }
+#undef SCG_NODES_CASES
 }
 
 }  // namespace scg

@@ -470,7 +470,8 @@ class SupplyChainVecEnv:
         if self.kernel == "staged":
             return f"scg::sc_step_staged_kernel<{maxd}>"
         if self.kernel == "nodes":
-            return f"scg::sc_step_nodes_kernel<{maxd}, {'true' if c.obs_f64 else 'false'}>"
+            return (f"scg::sc_step_nodes_kernel<{maxd}, {'true' if c.obs_f64 else 'false'}, "
+                    f"{'true' if self.build_info else 'false'}>")
         lds = 64 * len(self.spec.nodes) * self.spec.P * (12 * c.heap_capacity + 4)
         if lds > 64 * 1024:
             return f"scg::sc_step_kernel<{maxd}>"

@@ -18,9 +18,11 @@ def build():
         [os.path.join(REPO, "include", "scgpu.h")]
     if not (os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps)):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        tmp = f"{OUT}.{os.getpid()}.tmp"  # concurrent test workers: build aside, rename into place
         subprocess.run(["hipcc", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-Wno-pass-failed",
                         "--offload-arch=gfx950", "-I", os.path.join(REPO, "include"), "-I", CSRC,
-                        "-o", OUT, SRC], check=True)
+                        "-o", tmp, SRC], check=True)
+        os.replace(tmp, OUT)
     lib = ctypes.CDLL(OUT)
     lib.sch_episode.restype = ctypes.c_int
     lib.sch_episode_level.restype = ctypes.c_int

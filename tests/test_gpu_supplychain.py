@@ -378,9 +378,9 @@ def test_auto_kernel_symbols():
     node-staged kernel (config 4); kernel_symbol names what rocprofv3 reports."""
     import gym_supplychain_amd as gsa
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV)
-    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2, false>"
+    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2, false, false>"
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, build_info=True)
-    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2, false>"
+    assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2, false, true>"
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, kernel="lane")
     assert env.kernel == "lane" and env.kernel_symbol == "scg::sc_step_lds_kernel<2, 32>"
     cus = torch.cuda.get_device_properties(DEV).multi_processor_count

@@ -35,11 +35,13 @@ def build():
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     os.makedirs(os.path.dirname(EXE), exist_ok=True)
     # -fsanitize only for the host compilation (the device side has no sanitizer here)
+    tmp = f"{EXE}.{os.getpid()}.tmp"  # concurrent test workers: build aside, rename into place
     subprocess.run([hipcc, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-ffp-contract=off",
                     "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
                     "-Xarch_host", "-fno-sanitize-recover=all", "-Wno-pass-failed", "--offload-arch=gfx950",
                     "-I", os.path.join(REPO, "include"), "-I", CSRC, "-I", os.path.dirname(SRC),
-                    "-o", EXE, SRC], check=True)
+                    "-o", tmp, SRC], check=True)
+    os.replace(tmp, EXE)
     return EXE
 
 
