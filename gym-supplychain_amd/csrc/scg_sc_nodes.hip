@@ -109,8 +109,8 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   int32_t* ibtk = hsz + NP * 64;
   int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
   int32_t* amb = cost_k + NN * 64;
-  uint32_t* lmask = reinterpret_cast<uint32_t*>(amb + W * 64);  // ledger entry marks [NP][64]
-  float* act_t = reinterpret_cast<float*>(lmask + NP * 64);
+  uint64_t* lword = reinterpret_cast<uint64_t*>(amb + W * 64);  // ledger entry marks and types [NP][64]
+  float* act_t = reinterpret_cast<float*>(lword + NP * 64);
   // heaps and sizes in HBM (the batch's base pointers, column n); stocks in the LDS copy
   ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
   g.soff = lane;
@@ -118,10 +118,9 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   constexpr bool ledgers = LED;
   if (ledgers) {  // the nodes' entries to their slots (column n = base + n0 + soff), reduced below
     g.led_v = a.ledp_v + n0;
-    g.led_k = a.ledp_k + n0;
     g.led_stride = a.n;
-    g.led_mask = lmask + lane;
-    g.led_mask_stride = 64;
+    g.led_word = lword + lane;
+    g.led_word_stride = 64;
   }
   auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
   NSTAMP(0);
@@ -211,7 +210,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
       const int64_t at = q * a.n + n;
       double lv = a.led_v[at];
       int32_t lk = a.led_k[at];
-      sc_ledger_reduce(c, q, a.ledp_v + n, a.ledp_k + n, a.n, lmask + lane, 64, lv, lk);
+      sc_ledger_reduce(c, q, a.ledp_v + n, a.n, lword + lane, 64, lv, lk);
       if (autoreset) {
         if (a.led_fv) {
           a.led_fv[at] = lv;
@@ -255,7 +254,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
 size_t sc_nodes_lds_bytes(int n_nodes, int P, int H, int E, int W, int A, int O, int obs_bytes) {
   const size_t NP = static_cast<size_t>(n_nodes) * P;
   return 64 * ((NP * H + 2 * NP + E + n_nodes + 1) * 8 + static_cast<size_t>(O | 1) * obs_bytes +
-               (NP * H + 2 * NP + E + n_nodes + W) * 4 + static_cast<size_t>(A | 1) * 4);
+               (NP * H + NP + E + n_nodes + W) * 4 + NP * 8 + static_cast<size_t>(A | 1) * 4);
 }
 
 // Widest destination list the kernel is instantiated for (its split runs in registers).

@@ -404,8 +404,7 @@ int sc_check(const scg_sc_config* cfg, const scg_sc_state* st) {
     return fail(SCG_ERR_INVALID, "global env ids must fit in 32 bits");
   if (!st->stock || !st->heap_tk || !st->heap_val || !st->heap_size || !st->error_flags)
     return fail(SCG_ERR_INVALID, "state buffers stock/heap_tk/heap_val/heap_size/error_flags are required");
-  if (!st->ledger != !st->ledger_kind || !st->final_ledger != !st->final_ledger_kind ||
-      !st->ledger_part != !st->ledger_part_kind)
+  if (!st->ledger != !st->ledger_kind || !st->final_ledger != !st->final_ledger_kind)
     return fail(SCG_ERR_INVALID, "ledger values and kinds come in pairs");
   if (st->ledger && cfg->kernel == SCG_SC_KERNEL_LEVEL)
     return fail(SCG_ERR_INVALID, "build_info ledgers need the lane kernel");
@@ -453,7 +452,6 @@ ScArgs sc_args(const scg_sc_config* cfg, const scg_sc_state* st) {
   a.led_fv = st->final_ledger;
   a.led_fk = st->final_ledger_kind;
   a.ledp_v = st->ledger_part;
-  a.ledp_k = st->ledger_part_kind;
   a.n = st->n_envs;
   a.env_offset = st->env_offset;
   a.episode = st->episode;

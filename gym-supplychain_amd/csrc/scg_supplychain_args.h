@@ -29,8 +29,7 @@ struct ScArgs {
   int32_t* led_k;
   double* led_fv;    // terminal-step ledger on auto-reset
   int32_t* led_fk;
-  double* ledp_v;    // node-parallel kernel: the nodes' ledger entries of the step [NN*2*8*P][N]
-  int32_t* ledp_k;
+  double* ledp_v;    // node-parallel kernel: the nodes' ledger entry values of the step [NN*2*8*P][N]
   int64_t n;
   int64_t env_offset;
   uint32_t episode;

@@ -99,14 +99,15 @@ struct ScEnv {
   // them wave-uniform (SGPRs) instead of one 64-bit VGPR pair per pointer and lane.
   int64_t soff = 0;
   int64_t hoff = 0;
-  // Ledger entries by node (node-parallel kernel, where the nodes act at once): with led_mask
-  // set, sc_note stores node led_node's entry in its own slot ((node * 2 + part) * 8 + key) *
-  // P + p of led_v/led_k and marks it in the node's per-product word led_mask[(node * P + p) *
-  // led_mask_stride] (bit part * 8 + key); sc_ledger_reduce adds the marked slots to the
-  // ledger in node order afterwards, as _update_statistics does (:750-760).
+  // Ledger entries by node (node-parallel kernel, where the nodes act at once): with led_word
+  // set, sc_note stores the value of node led_node's entry in its own slot ((node * 2 + part)
+  // * 8 + key) * P + p of led_v, and marks it, with its NumPy type, in the node's per-product
+  // word led_word[(node * P + p) * led_word_stride] (bit pk = part * 8 + key, the type in
+  // bits 16 + 3 pk ..); sc_ledger_reduce adds the marked slots to the ledger in node order
+  // afterwards, as _update_statistics does (:750-760).
   int32_t led_node = 0;
-  uint32_t* led_mask = nullptr;
-  int64_t led_mask_stride = 0;
+  uint64_t* led_word = nullptr;
+  int64_t led_word_stride = 0;
 };
 
 // info['sc_episode'] categories in the reference's dict order (:416-417)
@@ -121,14 +122,14 @@ enum ScLedgerKey : int {
 // change neither value nor type of a sum, so they are skipped.
 __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int key, int p, Num cost, Num units) {
   if (!e.led_v) return;
-  if (e.led_mask) {  // by node: the slot of this node's entry, reduced in node order later
+  if (e.led_word) {  // by node: the slot of this node's entry, reduced in node order later
     const int64_t s0 = ((static_cast<int64_t>(e.led_node) * 2 * SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride + e.soff;
     const int64_t s1 = s0 + static_cast<int64_t>(SCG_SC_LEDGER_KEYS) * c.P * e.led_stride;
     e.led_v[s0] = cost.v;
-    e.led_k[s0] = np_kind_abi(cost.k);
     e.led_v[s1] = units.v;
-    e.led_k[s1] = np_kind_abi(units.k);
-    e.led_mask[(static_cast<int64_t>(e.led_node) * c.P + p) * e.led_mask_stride] |= (1u << key) | (1u << (8 + key));
+    const uint64_t k0 = static_cast<uint64_t>(np_kind_abi(cost.k)), k1 = static_cast<uint64_t>(np_kind_abi(units.k));
+    e.led_word[(static_cast<int64_t>(e.led_node) * c.P + p) * e.led_word_stride] |=
+        (uint64_t(1) << key) | (uint64_t(1) << (8 + key)) | (k0 << (16 + 3 * key)) | (k1 << (16 + 3 * (8 + key)));
     return;
   }
   const int64_t i0 = (static_cast<int64_t>(key) * c.P + p) * e.led_stride + e.soff;
@@ -143,24 +144,31 @@ __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int k
 
 // A node is about to act (node-parallel kernel with ledgers): its entries go to its slots.
 __host__ __device__ __forceinline__ void sc_led_begin_node(const ScCtx& c, ScEnv& e, int node) {
-  if (!e.led_v || !e.led_mask) return;
+  if (!e.led_v || !e.led_word) return;
   e.led_node = node;
-  for (int p = 0; p < c.P; ++p) e.led_mask[(static_cast<int64_t>(node) * c.P + p) * e.led_mask_stride] = 0;
+  for (int p = 0; p < c.P; ++p) e.led_word[(static_cast<int64_t>(node) * c.P + p) * e.led_word_stride] = 0;
 }
 
 // Ledger entry q = (part * 8 + key) * P + p of one env after the step: the nodes' marked
-// entries added in node order (:750-760) to (lv, lk). cv/ck: the slots (stride cstride);
-// mask: the per-(node, product) words (stride mstride).
-__host__ __device__ inline void sc_ledger_reduce(const ScCtx& c, int q, const double* cv, const int32_t* ck,
-                                                 int64_t cstride, const uint32_t* mask, int64_t mstride, double& lv,
-                                                 int32_t& lk) {
+// entries added in node order (:750-760) to (lv, lk). cv: the slot values (stride cstride);
+// words: the per-(node, product) marks and types (stride wstride). The slots of a batch of
+// nodes are requested together, so the chain of adds waits on memory once per batch.
+__host__ __device__ inline void sc_ledger_reduce(const ScCtx& c, int q, const double* cv, int64_t cstride,
+                                                 const uint64_t* words, int64_t wstride, double& lv, int32_t& lk) {
   const int p = q % c.P, pk = q / c.P;  // pk = part * 8 + key
-  const uint32_t bit = 1u << pk;
+  constexpr int kBatch = 8;
   Num acc{lv, np_kind_int(lk)};
-  for (int i = 0; i < c.n_nodes; ++i) {
-    if (!(mask[(static_cast<int64_t>(i) * c.P + p) * mstride] & bit)) continue;
-    const int64_t s = ((static_cast<int64_t>(i) * 2 * SCG_SC_LEDGER_KEYS + pk) * c.P + p) * cstride;
-    acc = np_add(acc, Num{cv[s], np_kind_int(ck[s])});
+  for (int i0 = 0; i0 < c.n_nodes; i0 += kBatch) {
+    double v[kBatch];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u)
+      if (i0 + u < c.n_nodes) v[u] = cv[((static_cast<int64_t>(i0 + u) * 2 * SCG_SC_LEDGER_KEYS + pk) * c.P + p) * cstride];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      if (i0 + u >= c.n_nodes) break;
+      const uint64_t w = words[(static_cast<int64_t>(i0 + u) * c.P + p) * wstride];
+      if ((w >> pk) & 1) acc = np_add(acc, Num{v[u], np_kind_int(static_cast<int>((w >> (16 + 3 * pk)) & 7))});
+    }
   }
   lv = acc.v;
   lk = np_kind_abi(acc.k);

@@ -163,8 +163,7 @@ class ScState(ctypes.Structure):
                 ("episode", ctypes.c_uint32), ("time_step", ctypes.c_int32)] + [
         (f, ctypes.c_void_p) for f in ("stock", "heap_tk", "heap_val", "heap_size", "episode_return",
                                        "final_return", "error_flags", "inbox_tk", "inbox_val", "ledger",
-                                       "ledger_kind", "final_ledger", "final_ledger_kind", "ledger_part",
-                                       "ledger_part_kind")]
+                                       "ledger_kind", "final_ledger", "final_ledger_kind", "ledger_part")]
 
 
 # Every symbol include/scgpu.h declares, with its ctypes signature.

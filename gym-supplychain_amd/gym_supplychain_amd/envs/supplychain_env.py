@@ -356,11 +356,10 @@ class SupplyChainVecEnv:
                 self._fled = torch.zeros(shape, dtype=torch.float64, device=dev)
                 self._fled_k = torch.zeros(shape, dtype=torch.int32, device=dev)
                 s.final_ledger, s.final_ledger_kind = self._fled.data_ptr(), self._fled_k.data_ptr()
-            if self.kernel == "nodes":  # each node's entries of a step [NN * 2 * 8 * P][N]
+            if self.kernel == "nodes":  # each node's entry values of a step [NN * 2 * 8 * P][N]
                 pshape = (NN * 2 * nat.SC_LEDGER_KEYS * P, n_envs)
                 self._led_part = torch.zeros(pshape, dtype=torch.float64, device=dev)
-                self._led_part_k = torch.zeros(pshape, dtype=torch.int32, device=dev)
-                s.ledger_part, s.ledger_part_kind = self._led_part.data_ptr(), self._led_part_k.data_ptr()
+                s.ledger_part = self._led_part.data_ptr()
             if not track_returns:
                 raise ValueError("build_info needs track_returns (sc_episode['rewards'])")
         self._st = s

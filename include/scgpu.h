@@ -403,12 +403,11 @@ typedef struct scg_sc_state {
   int32_t* ledger_kind;         /* [2 * 8 * P][N] */
   double* final_ledger;         /* [2 * 8 * P][N] optional */
   int32_t* final_ledger_kind;   /* [2 * 8 * P][N] optional */
-  /* Node-parallel kernel with ledgers: each node's entries of the step, [n_nodes * 2 * 8 * P][N]
-   * (slot ((node * 2 + part) * 8 + key) * P + p), added to the ledger in node order after the
-   * step (:750-760). Without them a ledger step of a SCG_SC_KERNEL_NODES config runs the lane
-   * kernel on the same state. */
+  /* Node-parallel kernel with ledgers: each node's entry values of the step, float64
+   * [n_nodes * 2 * 8 * P][N] (slot ((node * 2 + part) * 8 + key) * P + p; their NumPy types
+   * stay in LDS), added to the ledger in node order after the step (:750-760). Without it a
+   * ledger step of a SCG_SC_KERNEL_NODES config runs the lane kernel on the same state. */
   double* ledger_part;
-  int32_t* ledger_part_kind;
 } scg_sc_state;
 
 /* sizeof(scg_sc_node), sizeof(scg_sc_config), sizeof(scg_sc_state), to check FFI bindings. */

@@ -121,18 +121,17 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
       const int E = cfg->inbox_size > 0 ? cfg->inbox_size : 1;
       // ledgers by node, reduced in node order after the step (the kernel's ledger phase)
       std::vector<double> part_v(static_cast<size_t>(c.n_nodes) * LQ, -7.0);
-      std::vector<int32_t> part_k(part_v.size(), 99);
-      std::vector<uint32_t> marks(NP, 0xdeadbeefu);
+      std::vector<uint64_t> marks(NP, 0xdeadbeefdeadbeefull);
       if (ledger) {
         et.led_v = part_v.data();
-        et.led_k = part_k.data();
+        et.led_k = nullptr;
         et.led_stride = 1;
-        et.led_mask = marks.data();
-        et.led_mask_stride = 1;
+        et.led_word = marks.data();
+        et.led_word_stride = 1;
       }
       auto reduce_ledger = [&]() {
         if (!ledger) return;
-        for (int q = 0; q < LQ; ++q) scg::sc_ledger_reduce(c, q, part_v.data(), part_k.data(), 1, marks.data(), 1, led_v[q], led_k[q]);
+        for (int q = 0; q < LQ; ++q) scg::sc_ledger_reduce(c, q, part_v.data(), 1, marks.data(), 1, led_v[q], led_k[q]);
         std::memcpy(ledger + static_cast<int64_t>(t - 1) * LQ, led_v.data(), sizeof(double) * LQ);
         std::memcpy(ledger_kind + static_cast<int64_t>(t - 1) * LQ, led_k.data(), sizeof(int32_t) * LQ);
       };
