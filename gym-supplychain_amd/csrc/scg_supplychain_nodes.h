@@ -96,11 +96,14 @@ __host__ __device__ inline bool sc_recv_scan(const HeapView& h, int32_t sz, int 
 }
 
 // stage: heap (i, p) from the env's state into `lh` (its size into lsz), and what it
-// releases at t. Loads go out four at a time, as in the staged kernel.
+// releases at t. Loads go out SCG_NODES_STAGE_CHUNK at a time.
+#ifndef SCG_NODES_STAGE_CHUNK
+#define SCG_NODES_STAGE_CHUNK 4
+#endif
 __host__ __device__ inline bool sc_nodes_stage(const ScCtx& c, const ScEnv& g, const HeapView& lh, int32_t& lsz,
                                                int t, int i, int p, double& recv) {
   const HeapView gh = sc_heap(c, g, i, p);
-  constexpr int kChunk = 4;
+  constexpr int kChunk = SCG_NODES_STAGE_CHUNK;
   // the first chunk is requested with the size (one memory round instead of two for a heap
   // of at most kChunk entries; slots past the size are read but not used)
   HeapEntry b[kChunk];
