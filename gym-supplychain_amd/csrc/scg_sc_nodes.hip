@@ -39,15 +39,26 @@
 // barrier, 1 acted, 2 past the second, 3 heaps done, 7 past the third, 4 end) into a buffer of its own that scg_nodes_debug_stamps copies
 // out; nothing else reads it. In the product build NSTAMP is empty.
 #ifdef SCG_NODES_STAMPS
-constexpr int kNStampSlots = 8;
+// Slots 8 and 9 hold the real-time clock (100 MHz, one clock for the chip) at start and end,
+// 10 and 11 the wave's HW_ID and XCC_ID registers (where the block was placed).
+constexpr int kNStampSlots = 12;
 constexpr int kNStampWaves = 1 << 14;
 __device__ unsigned long long g_nodes_stamps[kNStampWaves * kNStampSlots];
 #define NSTAMP(k)                                                                                   \
   do {                                                                                              \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                                   \
+    const unsigned long long rt_ = ((k) == 0 || (k) == 4) ? __builtin_amdgcn_s_memrealtime() : 0ull; \
     const unsigned w_ = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;                        \
-    if ((threadIdx.x & 63u) == 0 && w_ < static_cast<unsigned>(kNStampWaves))                       \
-      g_nodes_stamps[w_ * kNStampSlots + (k)] = now_;                                               \
+    if ((threadIdx.x & 63u) == 0 && w_ < static_cast<unsigned>(kNStampWaves)) {                     \
+      unsigned long long* s_ = g_nodes_stamps + w_ * kNStampSlots;                                  \
+      s_[(k)] = now_;                                                                               \
+      if ((k) == 0) {                                                                               \
+        s_[8] = rt_;                                                                                \
+        s_[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                                         \
+        s_[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20);                                        \
+      }                                                                                             \
+      if ((k) == 4) s_[9] = rt_;                                                                    \
+    }                                                                                               \
   } while (0)
 #else
 #define NSTAMP(k)
@@ -90,7 +101,8 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   using ObsT = typename std::conditional<F64, double, float>::type;
   extern __shared__ __align__(16) unsigned char smem[];
   const ScCtx& c = a.c;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave index is wave-uniform: said so, node records are read with scalar loads
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n0 = static_cast<int64_t>(blockIdx.x) * 64;
   const int64_t n = n0 + lane;
   const int nb = a.n - n0 < 64 ? static_cast<int>(a.n - n0) : 64;  // envs of this block
@@ -131,21 +143,63 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   const NodesInbox in{ibtk + lane, ibval + lane, 64};
   const float* act = act_t + lane * Ap;
 
-  // stage: every heap of the wave's nodes, and the block's action rows into the tile
-  {
-    const float* src = a.act + n0 * c.A;
-    TileWalk tw(threadIdx.x, blockDim.x, c.A);
-    for (int q = threadIdx.x; q < nb * c.A; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
-  }
+  // stage, one memory round: every thread requests its share of the block's action rows
+  // (one contiguous span), every wave its node's stocks, heap sizes and the first kStage
+  // slots of each heap, wave 0 the episode returns; nothing is waited for until all are in
+  // flight. Then everything to LDS, the rest of a longer heap, and what each heap releases.
   bool bad = false;
-  if (live) {
+  {
+    constexpr int kAct = 4;  // action elements per thread per round
+    const float* src = a.act + n0 * c.A;
+    const int na = nb * c.A;
+    float av[kAct];
+#pragma unroll
+    for (int u = 0; u < kAct; ++u)
+      if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
+    const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
+    constexpr int kStage = 4;  // slots requested with the size (sc_nodes_stage); a longer heap costs a round more
     for (int i = w; i < NN; i += W)
       for (int p = 0; p < P; ++p) {
         const int hp = i * P + p;
-        stk[hp * 64 + lane] = a.stock[hp * a.n + n];
-        bad |= !sc_nodes_stage(c, g, lheap(hp), hsz[hp * 64 + lane], a.t, i, p, recv[hp * 64 + lane]);
+        if (!live) continue;
+        const int64_t r = static_cast<int64_t>(hp) * a.n + n;
+        const double st = a.stock[r];
+        const int32_t sz = a.size[r];
+        int32_t bt[kStage];
+        double bv[kStage];
+#pragma unroll
+        for (int u = 0; u < kStage; ++u)
+          if (u < H) {
+            bt[u] = a.tk[(static_cast<int64_t>(hp) * H + u) * a.n + n];
+            bv[u] = a.val[(static_cast<int64_t>(hp) * H + u) * a.n + n];
+          }
+        stk[hp * 64 + lane] = st;
+        hsz[hp * 64 + lane] = sz;
+        const HeapView lh = lheap(hp);
+#pragma unroll
+        for (int u = 0; u < kStage; ++u)
+          if (u < H) lh.put(u, HeapEntry{bt[u], bv[u]});
+        for (int j0 = kStage; j0 < sz; j0 += kStage) {  // a heap past kStage entries
+#pragma unroll
+          for (int u = 0; u < kStage; ++u)
+            if (j0 + u < sz) {
+              bt[u] = a.tk[(static_cast<int64_t>(hp) * H + j0 + u) * a.n + n];
+              bv[u] = a.val[(static_cast<int64_t>(hp) * H + j0 + u) * a.n + n];
+            }
+#pragma unroll
+          for (int u = 0; u < kStage; ++u)
+            if (j0 + u < sz) lh.put(j0 + u, HeapEntry{bt[u], bv[u]});
+        }
+        bad |= !sc_recv_scan(lh, sz, a.t, recv[hp * 64 + lane]);
       }
-    if (w == 0 && a.ep_ret) ret0[lane] = a.ep_ret[n];
+    {
+      TileWalk tw(threadIdx.x, blockDim.x, c.A);
+#pragma unroll
+      for (int u = 0; u < kAct; ++u, tw.next())
+        if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) act_t[tw.r * Ap + tw.k] = av[u];
+      for (int q = threadIdx.x + kAct * blockDim.x; q < na; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
+    }
+    if (w == 0 && live && a.ep_ret) ret0[lane] = r0;
   }
   amb[w * 64 + lane] = bad ? 1 : 0;
   NSTAMP(5);

@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--dump", default="", help="also save every wave's stamps to DUMP_<step>.npz")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -40,7 +41,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(0)
     for _ in range(10):
         env.step(torch.rand((a.envs, env.n_actions), generator=gen, device=dev) * 2 - 1)
-    buf = np.zeros((min(waves, 1 << 14), 8), dtype=np.uint64)
+    buf = np.zeros((min(waves, 1 << 14), 12), dtype=np.uint64)
     for s in range(a.steps):
         act = torch.rand((a.envs, env.n_actions), generator=gen, device=dev) * 2 - 1
         torch.cuda.synchronize()
@@ -60,6 +61,18 @@ def main():
                                 for k, n in enumerate(names)}
         wi = np.arange(len(st)) % W
         out["by_wave_p50"] = {n: [int(np.median(d[wi == w, k])) for w in range(W)] for k, n in enumerate(names)}
+        # real-time clock (100 MHz, one clock for the whole chip): the launch's timeline in us
+        rt = (st[:, 8:10] - st[:, 8].min()) / 100.0
+        blk = np.arange(len(st)) // W
+        bs, be = np.array([rt[blk == b, 0].min() for b in range(blk.max() + 1)]), \
+            np.array([rt[blk == b, 1].max() for b in range(blk.max() + 1)])
+        out["timeline_us"] = {"span": float(rt[:, 1].max()),
+                              "block_start_pct": [float(np.percentile(bs, q)) for q in (0, 25, 50, 75, 100)],
+                              "block_end_pct": [float(np.percentile(be, q)) for q in (0, 25, 50, 75, 100)],
+                              "block_dur_p50": float(np.median(be - bs)),
+                              "clock_mhz": float(np.median(d[:, 7] / np.maximum(rt[:, 1] - rt[:, 0], 1e-3)))}
+        if a.dump:
+            np.savez(f"{a.dump}_{s}.npz", stamps=st, W=W)
         print(json.dumps(out), flush=True)
 
 
