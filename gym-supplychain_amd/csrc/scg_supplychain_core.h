@@ -445,8 +445,33 @@ __host__ __device__ __forceinline__ void sc_split_d(const float (&vals)[MAXD], i
 
 // Action k of this env, denormalised like _denormalize_action (:697-698): (a + 1) / 2 on
 // a float32 array stays float32.
+__host__ __device__ __forceinline__ float sc_denorm(float a) { return (a + 1.0f) / 2.0f; }
 __host__ __device__ __forceinline__ Num sc_action(const float* raw, int k) {
-  return Num{static_cast<double>((raw[k] + 1.0f) / 2.0f), NK_F32};
+  return Num{static_cast<double>(sc_denorm(raw[k])), NK_F32};
+}
+
+// The D ship actions of a node and product, raw[base .. base + D), denormalised into
+// vals[0 .. D) (0 past D). Every load is unconditional (a clamped index stays inside the
+// row), so all of them are in flight before the first is waited for; guarded loads were
+// waited one by one (a memory round trip each on the staged kernel's HBM action rows).
+// K <= MAXD bounds the loads (a node with D <= K destinations loads K).
+template <int MAXD, int K>
+__host__ __device__ __forceinline__ void sc_ship_vals_k(const float* raw, int base, int D, float (&vals)[MAXD]) {
+  float x[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) x[i] = raw[base + (i < D ? i : 0)];
+#pragma unroll
+  for (int i = 0; i < MAXD; ++i) vals[i] = (i < K && i < D) ? sc_denorm(x[i < K ? i : 0]) : 0.0f;
+}
+template <int MAXD>
+__host__ __device__ __forceinline__ void sc_ship_vals(const float* raw, int base, int D, float (&vals)[MAXD]) {
+  if constexpr (MAXD > 8) {
+    if (D <= 8) {
+      sc_ship_vals_k<MAXD, 8>(raw, base, D, vals);
+      return;
+    }
+  }
+  sc_ship_vals_k<MAXD, MAXD>(raw, base, D, vals);
 }
 
 // receive (:220-228) for one heap: pop every entry due now, summed in a float64 array
@@ -521,8 +546,7 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         NumVec<MAXD> out;
         int rank[MAXD];
         bool cut = false;  // kLdsSplit: the split's amounts are in the scratch slots
-#pragma unroll
-        for (int i = 0; i < MAXD; ++i) vals[i] = i < D ? static_cast<float>(sc_action(act, nd.action_offset + a_i + i).v) : 0.0f;
+        sc_ship_vals<MAXD>(act, nd.action_offset + a_i, D, vals);
         if constexpr (Push::kLdsSplit) {
           cut = sc_split_scratch<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), push, rank);
         } else {
