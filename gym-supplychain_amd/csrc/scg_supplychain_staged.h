@@ -94,20 +94,32 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
   // heap size, the stock and the first inbox chunk are requested together up front.
   // (kChunk = 8 pushed the kernel to 256 VGPRs, one wave per SIMD, and ran slower.)
   constexpr int kChunk = 4;
+#ifndef SCG_STAGED_HCHUNK
+#define SCG_STAGED_HCHUNK 8
+#endif
+  constexpr int kHeapChunk = SCG_STAGED_HCHUNK;  // heap slots per memory round
   const int64_t q0 = nd.in_base + static_cast<int64_t>(p) * nd.in_deg;
   HeapEntry ib[kChunk];
 #pragma unroll
   for (int u = 0; u < kChunk; ++u)
     if (u < nd.in_deg) ib[u] = HeapEntry{in.tk[(q0 + u) * in.stride], in.val[(q0 + u) * in.stride]};
+  // the heap's first kHeapChunk slots are requested with its size (slots past the size are
+  // read but not used), the rest kHeapChunk at a time
+  HeapEntry b[kHeapChunk];
+#pragma unroll
+  for (int u = 0; u < kHeapChunk; ++u)
+    if (u < c.H) b[u] = gh.get(u);
   int32_t sz = gsz;
   SCG_ACC(7);
-  for (int j0 = 0; j0 < sz; j0 += kChunk) {
-    HeapEntry b[kChunk];
 #pragma unroll
-    for (int u = 0; u < kChunk; ++u)
+  for (int u = 0; u < kHeapChunk; ++u)
+    if (u < sz) lh.put(u, b[u]);
+  for (int j0 = kHeapChunk; j0 < sz; j0 += kHeapChunk) {
+#pragma unroll
+    for (int u = 0; u < kHeapChunk; ++u)
       if (j0 + u < sz) b[u] = gh.get(j0 + u);
 #pragma unroll
-    for (int u = 0; u < kChunk; ++u)
+    for (int u = 0; u < kHeapChunk; ++u)
       if (j0 + u < sz) lh.put(j0 + u, b[u]);
   }
   SCG_ACC(0);
