@@ -97,6 +97,49 @@ __host__ __device__ inline void py_siftup(const HeapView& h, int size, int pos) 
   py_siftup_item(h, size, pos, h.get(pos));
 }
 
+// heapq.heappop on a non-empty heap whose root the caller holds in registers (`root` =
+// heap[0]); returns the popped entry and leaves the new heap[0] in `root` (defined when the
+// heap is not empty afterwards), so a loop of pops reads no slot twice: the bottom-up
+// sift's first move puts the smaller child at the root, and the re-seated last entry lands
+// there only if it climbs all the way back.
+__host__ __device__ inline HeapEntry py_heappop_root(const HeapView& h, int32_t& size, HeapEntry& root) {
+  --size;
+  const HeapEntry last = h.get(size);
+  const HeapEntry ret = root;
+  if (size == 0) return last;
+  int pos = 0, childpos = 1;
+  bool moved = false;
+  while (childpos < size) {
+    const int rightpos = childpos + 1;
+    HeapEntry child = h.get(childpos);
+    if (rightpos < size) {
+      const HeapEntry right = h.get(rightpos);
+      if (!he_less(child, right)) {
+        childpos = rightpos;
+        child = right;
+      }
+    }
+    h.put(pos, child);
+    if (!moved) root = child;
+    moved = true;
+    pos = childpos;
+    childpos = 2 * pos + 1;
+  }
+  while (pos > 0) {  // _siftdown(heap, 0, pos) of `last`
+    const int parentpos = (pos - 1) >> 1;
+    const HeapEntry parent = h.get(parentpos);
+    if (he_less(last, parent)) {
+      h.put(pos, parent);
+      pos = parentpos;
+      continue;
+    }
+    break;
+  }
+  h.put(pos, last);
+  if (pos == 0) root = last;
+  return ret;
+}
+
 // heapq.heappush. Returns false (and pushes nothing) when the heap is full.
 __host__ __device__ inline bool py_heappush(const HeapView& h, int32_t& size, int cap, const HeapEntry& e) {
   if (size >= cap) return false;

@@ -689,14 +689,21 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   cfg->level_staged = 0;
   // auto: the node-parallel kernel when every node gets a wave of its own and two blocks
   // fit a CU's LDS (sc-2perstage-v0: 48 us against the LDS lane kernel's 68 us per step on
-  // MI355X); else the lane kernel with every heap in LDS when a block's heaps
+  // MI355X), or one block does and nothing but the staged kernel would take
+  // the chain; else the lane kernel with every heap in LDS when a block's heaps
   // fit; else the node-staged kernel when the chain qualifies (measured faster than the lane
   // kernel on HBM heaps); else the lane kernel on HBM heaps
+  // One block per CU (a block's LDS past half the CU's) still beats the node-staged kernel:
+  // sc-2perstage-multiproduct-v0 at 65,536 envs 92.5 against 126 us (profiles/r03x_*), so
+  // the node-parallel kernel is also taken then, unless the lane kernel's heaps fit LDS
+  // (a case not measured at one block per CU).
   if (want == SCG_SC_KERNEL_AUTO && NN <= sc_nodes_waves(NN) && maxd <= sc_nodes_max_dests() && H <= 64) {
     std::vector<scg_sc_node> probe(nodes, nodes + NN);
     const int entries = sc_inbox_layout(cfg, probe.data());
-    if (entries >= 0 && 2 * sc_nodes_lds_bytes(NN, P, H, entries, sc_nodes_waves(NN), n_act, cfg->n_obs,
-                                               cfg->obs_f64 ? 8 : 4) <= sc_nodes_lds_max())
+    const size_t lds = entries < 0 ? 0
+                                   : sc_nodes_lds_bytes(NN, P, H, entries, sc_nodes_waves(NN), n_act, cfg->n_obs,
+                                                        cfg->obs_f64 ? 8 : 4);
+    if (entries >= 0 && (2 * lds <= sc_nodes_lds_max() || (lds <= sc_nodes_lds_max() && sc_lds_bytes(cfg) > kScLdsMax)))
       want = SCG_SC_KERNEL_NODES;
   }
   if (want == SCG_SC_KERNEL_AUTO && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {

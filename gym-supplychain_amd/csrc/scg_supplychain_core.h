@@ -290,7 +290,10 @@ __host__ __device__ __forceinline__ void sc_push(const ScCtx& c, ScEnv& e, int n
 struct DirectPush {
   static constexpr bool kUnroll = false;
   static constexpr bool kLdsSplit = false;  // see sc_split_scratch
+  static constexpr bool kClearInAct = false;  // see StagedInbox::noship
   __host__ __device__ Num scratch_get(int) const { return pyint(0); }
+  __host__ __device__ void noship(const ScCtx&, int, int, int) const {}
+  __host__ __device__ void noship_all(const ScCtx&, int, int) const {}
   __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv& e, int /*src*/, int /*d*/, int dest, int p,
                                                 int32_t time, Num amount) const {
     sc_push(c, e, dest, p, time, amount);
@@ -475,9 +478,19 @@ __host__ __device__ __forceinline__ void sc_ship_vals(const float* raw, int base
 }
 
 // receive (:220-228) for one heap: pop every entry due now, summed in a float64 array
+#ifndef SCG_RECV_ROOT
+#define SCG_RECV_ROOT 1
+#endif
 __host__ __device__ __forceinline__ double sc_receive(const HeapView& h, int32_t& sz, int t) {
   double recv = 0.0;
+#if SCG_RECV_ROOT
+  // the root travels in registers from pop to pop (py_heappop_root): no slot read twice
+  if (sz == 0) return recv;
+  HeapEntry root = h.get(0);
+  while (sz > 0 && he_time(root.tk) == t) recv = recv + py_heappop_root(h, sz, root).v;
+#else
   while (sz > 0 && h.time_at(0) == t) recv = recv + py_heappop(h, sz).v;
+#endif
   return recv;
 }
 
@@ -538,7 +551,10 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
     const int lt_base = lt_i;
     const bool factory = nd.processing_capacity > 0;
     for (int p = 0; p < P; ++p) {
-      if (!(nd.stock_capacity[p] > 0)) continue;  // no SHIP action for this product
+      if (!(nd.stock_capacity[p] > 0)) {  // no SHIP action for this product
+        if constexpr (Push::kClearInAct) push.noship_all(c, ni, p);
+        continue;
+      }
       Num over_ship = pyint(0), over_proc = pyint(0);
       const Num material = f64(sc_stock(c, e, ni, p));
       if (np_lt(pyint(0), material)) {
@@ -588,6 +604,8 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
           leaving = np_add(leaving, o);
           if (np_lt(pyint(0), snt))
             push.ship(c, e, ni, i, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
+          else if constexpr (Push::kClearInAct)
+            push.noship(c, ni, i, p);
           ship_cost = np_add(ship_cost, np_mul(snt, pyint(nd.dest_costs[p][i])));
           ship_units = np_add(ship_units, snt);  // sum(amounts_to_ship) (:356)
         };
@@ -608,6 +626,8 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
         }
         cost = np_add(cost, ship_cost);
         sc_note(c, e, LK_SHIP, p, ship_cost, ship_units);
+      } else {
+        if constexpr (Push::kClearInAct) push.noship_all(c, ni, p);
       }
       const Num pen_proc = np_mul(pyint(c.pen_proc), over_proc);  // :361
       cost = np_add(cost, pen_proc);

@@ -42,7 +42,10 @@ struct NodesInbox {
 
   static constexpr bool kUnroll = true;
   static constexpr bool kLdsSplit = false;
+  static constexpr bool kClearInAct = false;  // cleared before the act
   __host__ __device__ Num scratch_get(int) const { return pyint(0); }
+  __host__ __device__ void noship(const ScCtx&, int, int, int) const {}
+  __host__ __device__ void noship_all(const ScCtx&, int, int) const {}
   __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv&, int src, int d, int /*dest*/, int p,
                                                 int32_t time, Num amount) const {
     ScNode& nd = c.nodes[src];

@@ -48,6 +48,13 @@ struct StagedInbox {
 
   static constexpr bool kUnroll = true;  // a store per destination
   static constexpr bool kLdsSplit = true;
+#ifndef SCG_STAGED_NOSHIP
+#define SCG_STAGED_NOSHIP 1
+#endif
+  // Entries the act does not ship to are marked empty by the act itself (noship /
+  // noship_all: one store per destination and product in all), instead of a clear of the
+  // node's every entry before it acts followed by the shipments' stores over most of them.
+  static constexpr bool kClearInAct = SCG_STAGED_NOSHIP != 0;
   __host__ __device__ __forceinline__ void scratch_put_value(int s, float v) const {
     scr.tk[s * scr.stride] = sc_f2i(v);
   }
@@ -65,6 +72,14 @@ struct StagedInbox {
     const int64_t q = nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d];
     tk[q * stride] = he_pack(time, amount.k);
     val[q * stride] = amount.v;
+  }
+  __host__ __device__ __forceinline__ void noship(const ScCtx& c, int src, int d, int p) const {
+    ScNode& nd = c.nodes[src];
+    tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = -1;
+  }
+  __host__ __device__ __forceinline__ void noship_all(const ScCtx& c, int src, int p) const {
+    ScNode& nd = c.nodes[src];
+    for (int d = 0; d < nd.n_dests; ++d) tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = -1;
   }
   // node src ships nothing this step unless its act writes an entry
   __host__ __device__ __forceinline__ void clear(const ScCtx& c, int src) const {
@@ -172,7 +187,7 @@ __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const
     ScNode& nd = c.nodes[i];
     int a_i = 0, lt_i = 0;
     for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out, scg_acc_);
-    if (!nd.last_level) in.clear(c, i);
+    if (!StagedInbox::kClearInAct && !nd.last_level) in.clear(c, i);
     SCG_ACC(7);
     total = np_add(total, sc_node_act<MAXD, StagedInbox, true>(c, g, ltc, dmc, i, act, t, in));
     SCG_ACC(5);

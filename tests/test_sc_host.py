@@ -215,12 +215,17 @@ def test_recv_scan_flags_float32_ties():
 
 def test_auto_kernel_choice():
     """kernel='auto' (scg_sc_prepare, host only): the node-parallel kernel when every node
-    gets a wave and two blocks fit a CU's LDS (2-per-stage), the lane kernel with heaps in
-    LDS when only a block's heaps fit (2-per-stage with max lead time 4: heaps of 10), the
-    node-staged kernel on the wide ntom chain."""
+    gets a wave and two blocks fit a CU's LDS (2-per-stage), or one block does where the lane
+    kernel's heaps would not fit LDS (the two-product 2-per-stage chain), the lane kernel
+    with heaps in LDS when only a block's heaps fit (2-per-stage with max lead time 4: heaps
+    of 10), the node-staged kernel on the wide ntom chain and the 3-product chain."""
     from gym_supplychain_amd import _native as nat
     _, c, _, _ = _setup(load_sc("2perstage"), nat.SC_KERNEL_AUTO)
     assert c.kernel == nat.SC_KERNEL_NODES and c.inbox_size > 0 and c.group == 8
+    _, c, _, _ = _setup(load_sc("multiproduct"), nat.SC_KERNEL_AUTO)
+    assert c.kernel == nat.SC_KERNEL_NODES and c.n_products == 2 and c.group == 8
+    _, c, _, _ = _setup(load_sc("byproduct"), nat.SC_KERNEL_AUTO)
+    assert c.kernel == nat.SC_KERNEL_STAGED and c.n_products == 3
     _, c, _, _ = _setup(load_sc("2perstage_stoch"), nat.SC_KERNEL_AUTO)
     assert c.kernel == nat.SC_KERNEL_LANE and c.inbox_size == 0
     _, c, _, _ = _setup(load_sc("ntom"), nat.SC_KERNEL_AUTO)

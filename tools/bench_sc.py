@@ -27,6 +27,11 @@ HBM_PEAK_GBS = 8000.0
 SCENARIOS = {
     "2perstage": dict(env_id="sc-2perstage-v0", kwargs={}, n_envs=65536, bytes_per_env_step=1148,
                       baseline_cfg="configs[2]"),
+    # not a BASELINE config: the two-product 2-per-stage chain (4 registered ids), whose
+    # node-parallel block needs a whole CU's LDS; SURVEY §8(d)'s formula with H = 4:
+    # 2 x 16 x (8 + 4 x 12 + 4) + 28 x 4 + 53 x 4 + 8 + 2 x 2 x 8
+    "2perstage_mp": dict(env_id="sc-2perstage-multiproduct-v0", kwargs={}, n_envs=65536, bytes_per_env_step=2284,
+                         baseline_cfg="none; 2-product sc-2perstage"),
     "ntom": dict(env_id="sc-Nperstage-multiproduct-v0", kwargs=dict(nodes_per_echelon=[8, 8, 8, 16]),
                  n_envs=262144, bytes_per_env_step=36108, baseline_cfg="configs[3]"),
 }
@@ -146,7 +151,7 @@ def run(name, steps, warmup, n_envs, cpu, kernel="auto", build_info=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scenario", default="both", choices=["2perstage", "ntom", "both"])
+    ap.add_argument("--scenario", default="both", choices=["2perstage", "2perstage_mp", "ntom", "both"])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=0)
@@ -157,7 +162,7 @@ def main():
     for name in (["2perstage", "ntom"] if a.scenario == "both" else [a.scenario]):
         kernels = [a.kernel]
         if a.kernel in ("all", "both"):  # the node-parallel kernel only takes chains whose block fits LDS
-            kernels = ["lane", "level", "staged"] + (["nodes"] if name == "2perstage" else [])
+            kernels = ["lane", "level", "staged"] + (["nodes"] if name != "ntom" else [])
         for k in kernels:
             run(name, a.steps, a.warmup, a.envs, not a.no_cpu_baseline and k == kernels[-1], k, a.build_info)
 
