@@ -29,11 +29,22 @@ __host__ __device__ __forceinline__ int32_t he_pack(int32_t time, int kind) { re
 // Python tuple (t1, a1) < (t2, a2): times first; on equal times the amounts (equal amounts
 // are not less, and np_lt already says so). Evaluated without branches: inside a sift loop
 // each early return was a divergent branch with its exec-mask bookkeeping.
+//
+// kPlain: the caller knows that neither entry is a Python int or float (kind codes 0 and 1).
+// NumPy compares at float32 precision only when the kinds OR to float32, i.e. a float32
+// against a float32 (both exact in a double: the same answer as comparing the doubles) or
+// against a Python scalar; without the latter the tuple order is the doubles' order, one
+// compare instead of the kind lattice's conversions and selects.
+template <bool kPlain = false>
 __host__ __device__ __forceinline__ bool he_less(const HeapEntry& x, const HeapEntry& y) {
   const int32_t tx = he_time(x.tk), ty = he_time(y.tk);
+  if constexpr (kPlain) return (tx < ty) | ((tx == ty) & (x.v < y.v));
   const Num ax{x.v, he_kind(x.tk)}, ay{y.v, he_kind(y.tk)};
   return (tx < ty) | ((tx == ty) & np_lt(ax, ay));
 }
+
+// An entry he_less<true> may compare: its kind is neither a Python int nor a Python float.
+__host__ __device__ __forceinline__ bool he_plain(int32_t tk) { return (tk & 6) != 0; }
 
 struct HeapView {
   int32_t* tk;
@@ -53,11 +64,12 @@ struct HeapView {
 // entries being moved in registers the same way, so each heap slot is read once per sift
 // level (the heap is in LDS in every kernel but the lane one on HBM heaps: these reads are
 // a chain of dependent latencies).
+template <bool kPlain = false>
 __host__ __device__ inline void py_siftdown_item(const HeapView& h, int startpos, int pos, const HeapEntry& item) {
   while (pos > startpos) {
     const int parentpos = (pos - 1) >> 1;
     const HeapEntry parent = h.get(parentpos);
-    if (he_less(item, parent)) {
+    if (he_less<kPlain>(item, parent)) {
       h.put(pos, parent);
       pos = parentpos;
       continue;
@@ -102,6 +114,7 @@ __host__ __device__ inline void py_siftup(const HeapView& h, int size, int pos) 
 // heap is not empty afterwards), so a loop of pops reads no slot twice: the bottom-up
 // sift's first move puts the smaller child at the root, and the re-seated last entry lands
 // there only if it climbs all the way back.
+template <bool kPlain = false>
 __host__ __device__ inline HeapEntry py_heappop_root(const HeapView& h, int32_t& size, HeapEntry& root) {
   --size;
   const HeapEntry last = h.get(size);
@@ -114,7 +127,7 @@ __host__ __device__ inline HeapEntry py_heappop_root(const HeapView& h, int32_t&
     HeapEntry child = h.get(childpos);
     if (rightpos < size) {
       const HeapEntry right = h.get(rightpos);
-      if (!he_less(child, right)) {
+      if (!he_less<kPlain>(child, right)) {
         childpos = rightpos;
         child = right;
       }
@@ -128,7 +141,7 @@ __host__ __device__ inline HeapEntry py_heappop_root(const HeapView& h, int32_t&
   while (pos > 0) {  // _siftdown(heap, 0, pos) of `last`
     const int parentpos = (pos - 1) >> 1;
     const HeapEntry parent = h.get(parentpos);
-    if (he_less(last, parent)) {
+    if (he_less<kPlain>(last, parent)) {
       h.put(pos, parent);
       pos = parentpos;
       continue;

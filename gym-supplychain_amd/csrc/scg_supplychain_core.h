@@ -481,13 +481,14 @@ __host__ __device__ __forceinline__ void sc_ship_vals(const float* raw, int base
 #ifndef SCG_RECV_ROOT
 #define SCG_RECV_ROOT 1
 #endif
+template <bool kPlain = false>
 __host__ __device__ __forceinline__ double sc_receive(const HeapView& h, int32_t& sz, int t) {
   double recv = 0.0;
 #if SCG_RECV_ROOT
   // the root travels in registers from pop to pop (py_heappop_root): no slot read twice
   if (sz == 0) return recv;
   HeapEntry root = h.get(0);
-  while (sz > 0 && he_time(root.tk) == t) recv = recv + py_heappop_root(h, sz, root).v;
+  while (sz > 0 && he_time(root.tk) == t) recv = recv + py_heappop_root<kPlain>(h, sz, root).v;
 #else
   while (sz > 0 && h.time_at(0) == t) recv = recv + py_heappop(h, sz).v;
 #endif

@@ -113,6 +113,9 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 #define SCG_STAGED_HCHUNK 8
 #endif
   constexpr int kHeapChunk = SCG_STAGED_HCHUNK;  // heap slots per memory round
+#ifndef SCG_STAGED_PLAIN
+#define SCG_STAGED_PLAIN 1
+#endif
   const int64_t q0 = nd.in_base + static_cast<int64_t>(p) * nd.in_deg;
   HeapEntry ib[kChunk];
 #pragma unroll
@@ -126,16 +129,23 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
     if (u < c.H) b[u] = gh.get(u);
   int32_t sz = gsz;
   SCG_ACC(7);
+  bool plain = true;  // no Python int or float amount in the heap (he_less<true> applies)
 #pragma unroll
   for (int u = 0; u < kHeapChunk; ++u)
-    if (u < sz) lh.put(u, b[u]);
+    if (u < sz) {
+      lh.put(u, b[u]);
+      plain &= he_plain(b[u].tk);
+    }
   for (int j0 = kHeapChunk; j0 < sz; j0 += kHeapChunk) {
 #pragma unroll
     for (int u = 0; u < kHeapChunk; ++u)
       if (j0 + u < sz) b[u] = gh.get(j0 + u);
 #pragma unroll
     for (int u = 0; u < kHeapChunk; ++u)
-      if (j0 + u < sz) lh.put(j0 + u, b[u]);
+      if (j0 + u < sz) {
+        lh.put(j0 + u, b[u]);
+        plain &= he_plain(b[u].tk);
+      }
   }
   SCG_ACC(0);
   for (int k0 = 0; k0 < nd.in_deg; k0 += kChunk) {
@@ -147,10 +157,22 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
     }
 #pragma unroll
     for (int u = 0; u < kChunk; ++u)  // in source order (:347)
-      if (k0 + u < nd.in_deg && ib[u].tk >= 0 && !py_heappush(lh, sz, c.H, ib[u])) g.overflow = 1;
+      if (k0 + u < nd.in_deg && ib[u].tk >= 0) {
+        plain &= he_plain(ib[u].tk);
+        if (!py_heappush(lh, sz, c.H, ib[u])) g.overflow = 1;
+      }
   }
   SCG_ACC(1);
-  st = st0 + sc_receive(lh, sz, t);
+  // the pops, the phase's longest part, compare the doubles when no lane of the wave holds
+  // a Python int or float amount (a wave-uniform choice, so no lane runs both bodies)
+#if SCG_STAGED_PLAIN && defined(__HIP_DEVICE_COMPILE__)
+  if (__all(plain))
+    st = st0 + sc_receive<true>(lh, sz, t);
+  else
+    st = st0 + sc_receive(lh, sz, t);
+#else
+  st = st0 + (SCG_STAGED_PLAIN && plain ? sc_receive<true>(lh, sz, t) : sc_receive(lh, sz, t));
+#endif
   SCG_ACC(2);
   if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) {
     const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));
