@@ -207,7 +207,9 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
 #ifndef SCG_STAGED_WPE
 #define SCG_STAGED_WPE 0  // 0: the compiler's choice
 #endif
-template <int MAXD>
+// LED: build_info ledgers kept (a separate instantiation: without it every ledger note,
+// and the per-destination unit sums only ledgers read, compile away).
+template <int MAXD, bool LED>
 __global__ __launch_bounds__(kScBlock)
 #if SCG_STAGED_WPE
 __attribute__((amdgpu_waves_per_eu(SCG_STAGED_WPE)))
@@ -222,6 +224,10 @@ void sc_step_staged_kernel(const ScArgs a) {
   const int slots = c.H > MAXD ? c.H : MAXD;  // sc_staged_lds_bytes
   int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
   ScEnv g = env_view(a, n, a.episode);
+  if constexpr (!LED) {
+    g.led_v = nullptr;
+    g.led_k = nullptr;
+  }
   const HeapView lh{ltk + lane, lval + lane, kScBlock};
   const StagedInbox in{a.inbox_tk + n, a.inbox_val + n, a.n, lh};
   const bool terminal = a.flags & 1;
@@ -808,11 +814,17 @@ int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float* action,
       return fail(SCG_ERR_INVALID, "the staged kernel needs the inbox buffers [inbox_size][N]");
     const size_t slds = sc_staged_lds_bytes(cfg);
     switch (sc_maxd_bucket(cfg->max_dests)) {
-      case 2: hipLaunchKernelGGL(sc_step_staged_kernel<2>, grid, dim3(kScBlock), slds, s, a); break;
-      case 4: hipLaunchKernelGGL(sc_step_staged_kernel<4>, grid, dim3(kScBlock), slds, s, a); break;
-      case 8: hipLaunchKernelGGL(sc_step_staged_kernel<8>, grid, dim3(kScBlock), slds, s, a); break;
-      case 16: hipLaunchKernelGGL(sc_step_staged_kernel<16>, grid, dim3(kScBlock), slds, s, a); break;
-      default: hipLaunchKernelGGL(sc_step_staged_kernel<32>, grid, dim3(kScBlock), slds, s, a); break;
+#define SCG_STAGED_LAUNCH(D)                                                                                   \
+  if (a.led_v)                                                                                                 \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_staged_kernel<D, true>), grid, dim3(kScBlock), slds, s, a);    \
+  else                                                                                                         \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_staged_kernel<D, false>), grid, dim3(kScBlock), slds, s, a)
+      case 2: SCG_STAGED_LAUNCH(2); break;
+      case 4: SCG_STAGED_LAUNCH(4); break;
+      case 8: SCG_STAGED_LAUNCH(8); break;
+      case 16: SCG_STAGED_LAUNCH(16); break;
+      default: SCG_STAGED_LAUNCH(32); break;
+#undef SCG_STAGED_LAUNCH
     }
   } else if (cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST) {
     return fail(SCG_ERR_INVALID, "lane kernel needs the env-fastest layout");

@@ -702,9 +702,16 @@ __host__ __device__ __forceinline__ void sc_observe_stock(const ScCtx& c, const 
 struct NoVisit {
   __host__ __device__ __forceinline__ void operator()(int, const HeapEntry&) const {}
 };
+template <class V>
+inline constexpr bool kNoVisit = false;
+template <>
+inline constexpr bool kNoVisit<NoVisit> = true;
 
 // node i, product p: avg_leadtime in-transit bins over heap h of size sz (:445-461). The
 // walk reads every entry once, in storage order; visit(k, entry) sees each of them.
+#ifndef SCG_BINS_BATCH
+#define SCG_BINS_BATCH 1
+#endif
 template <class Sink, class Visit = NoVisit>
 __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& h, int32_t sz, int t, int i, int p,
                                                 Sink& out, const Visit& visit = Visit()) {
@@ -717,6 +724,42 @@ __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& 
     for (int b = first; b <= last; ++b) out(o++, sc_obs_norm(0.0));
     return;
   }
+#if SCG_BINS_BATCH
+  if constexpr (!kNoVisit<Visit>) {  // the kernels' step walks (their copy-back rides on it)
+    // The same walk as one pass over the entries in storage order with a bin cursor that
+    // only moves forward: entry k closes the bins before its time (while the cursor is short
+    // of the last bin), then joins the cursor's bin, so every bin sums the same entries in
+    // the same order. The entries are read kBatch at a time, all requested before the first
+    // is tested (the walk below waits on each slot's read before deciding on the next).
+    constexpr int kBatch = 8;
+    int when = first;
+    Num bin = pyint(0);
+    for (int k0 = 0; k0 < sz; k0 += kBatch) {
+      HeapEntry b[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u)
+        if (k0 + u < sz) b[u] = h.get(k0 + u);
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u)
+        if (k0 + u < sz) {
+          visit(k0 + u, b[u]);
+          const int32_t tm = he_time(b[u].tk);
+          while (when < last && tm != when) {
+            out(o++, sc_obs_norm(np_div(bin, pyint(nd.max_ship[p])).v));
+            bin = pyint(0);
+            ++when;
+          }
+          bin = np_add(bin, Num{b[u].v, he_kind(b[u].tk)});
+        }
+    }
+    for (; when < last; ++when) {
+      out(o++, sc_obs_norm(np_div(bin, pyint(nd.max_ship[p])).v));
+      bin = pyint(0);
+    }
+    out(o, sc_obs_norm(np_div(bin, pyint(nd.max_ship[p] * (c.max_lt - (last - first)))).v));
+    return;
+  }
+#endif
   int k = 0;
   for (int when = first; when < last; ++when) {
     Num bin = pyint(0);

@@ -164,8 +164,9 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
   if (receive) {
     double& st = sc_stock(c, g, i, p);
     st = st + sc_receive(lh, sz, t);
-  } else {
-    while (sz > 0 && lh.time_at(0) == t) py_heappop(lh, sz);
+  } else if (sz > 0) {  // the root travels in registers from pop to pop (py_heappop_root)
+    HeapEntry root = lh.get(0);
+    while (sz > 0 && he_time(root.tk) == t) py_heappop_root(lh, sz, root);
   }
   if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) {
     const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));

@@ -467,7 +467,7 @@ class SupplyChainVecEnv:
         if self.kernel == "level":
             return f"scg::sc_level_kernel<{maxd}, {'true' if c.level_staged else 'false'}>"
         if self.kernel == "staged":
-            return f"scg::sc_step_staged_kernel<{maxd}>"
+            return f"scg::sc_step_staged_kernel<{maxd}, {'true' if self.build_info else 'false'}>"
         if self.kernel == "nodes":
             return (f"scg::sc_step_nodes_kernel<{maxd}, {'true' if c.obs_f64 else 'false'}, "
                     f"{'true' if self.build_info else 'false'}>")

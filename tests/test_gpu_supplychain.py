@@ -389,7 +389,7 @@ def test_auto_kernel_symbols():
     env = gsa.make_vec("sc-2perstage-multiproduct-v0", 64, device=DEV)  # one block per CU
     assert env.kernel == "nodes" and env.kernel_symbol == "scg::sc_step_nodes_kernel<2, false, false>"
     env = gsa.make_vec("sc-Nperstage-multiproduct-v0", 64, device=DEV, nodes_per_echelon=[8, 8, 8, 16])
-    assert env.kernel == "staged" and env.kernel_symbol == "scg::sc_step_staged_kernel<16>"
+    assert env.kernel == "staged" and env.kernel_symbol == "scg::sc_step_staged_kernel<16, false>"
     env = gsa.make_vec("sc-2perstage-v0", 64, device=DEV, kernel="level")
     assert env.kernel_symbol.startswith("scg::sc_level_kernel<2, ")
 
