@@ -478,20 +478,13 @@ __host__ __device__ __forceinline__ void sc_ship_vals(const float* raw, int base
 }
 
 // receive (:220-228) for one heap: pop every entry due now, summed in a float64 array
-#ifndef SCG_RECV_ROOT
-#define SCG_RECV_ROOT 1
-#endif
 template <bool kPlain = false>
 __host__ __device__ __forceinline__ double sc_receive(const HeapView& h, int32_t& sz, int t) {
   double recv = 0.0;
-#if SCG_RECV_ROOT
   // the root travels in registers from pop to pop (py_heappop_root): no slot read twice
   if (sz == 0) return recv;
   HeapEntry root = h.get(0);
   while (sz > 0 && he_time(root.tk) == t) recv = recv + py_heappop_root<kPlain>(h, sz, root).v;
-#else
-  while (sz > 0 && h.time_at(0) == t) recv = recv + py_heappop(h, sz).v;
-#endif
   return recv;
 }
 
@@ -709,9 +702,6 @@ inline constexpr bool kNoVisit<NoVisit> = true;
 
 // node i, product p: avg_leadtime in-transit bins over heap h of size sz (:445-461). The
 // walk reads every entry once, in storage order; visit(k, entry) sees each of them.
-#ifndef SCG_BINS_BATCH
-#define SCG_BINS_BATCH 1
-#endif
 template <class Sink, class Visit = NoVisit>
 __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& h, int32_t sz, int t, int i, int p,
                                                 Sink& out, const Visit& visit = Visit()) {
@@ -724,7 +714,6 @@ __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& 
     for (int b = first; b <= last; ++b) out(o++, sc_obs_norm(0.0));
     return;
   }
-#if SCG_BINS_BATCH
   if constexpr (!kNoVisit<Visit>) {  // the kernels' step walks (their copy-back rides on it)
     // The same walk as one pass over the entries in storage order with a bin cursor that
     // only moves forward: entry k closes the bins before its time (while the cursor is short
@@ -759,7 +748,6 @@ __host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& 
     out(o, sc_obs_norm(np_div(bin, pyint(nd.max_ship[p] * (c.max_lt - (last - first)))).v));
     return;
   }
-#endif
   int k = 0;
   for (int when = first; when < last; ++when) {
     Num bin = pyint(0);

@@ -400,6 +400,8 @@ FULL_CASES = {
     "2perstage_nodes": ("sc-2perstage-v0", 65536, {"kernel": "nodes"}),
     "2perstage_stoch_nodes": ("sc-2perstage-v0", 65536, {"kernel": "nodes", "stochastic_leadtimes": True,
                                                           "avg_leadtime": 2, "max_leadtime": 4}),
+    # two products: the auto kernel is the node-parallel one at one block per CU
+    "2perstage_multiproduct": ("sc-2perstage-multiproduct-v0", 65536, {}),
     "ntom": ("sc-Nperstage-multiproduct-v0", 262144, dict(nodes_per_echelon=[8, 8, 8, 16])),
     "ntom_stoch": ("sc-Nperstage-multiproduct-v0", 262144,
                    dict(nodes_per_echelon=[8, 8, 8, 16], stochastic_leadtimes=True, avg_leadtime=2, max_leadtime=4)),
