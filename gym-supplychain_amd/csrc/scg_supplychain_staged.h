@@ -95,7 +95,7 @@ struct StagedInbox {
 // lead-time cursor `lt_i` and supply-action index `a_i` advanced as act advances them);
 // then, the heap being final for the step, its in-transit bins (:445-461). Heap storage
 // order is the reference's: the same pushes and pops happen in the same order.
-template <int HCHUNK, class Sink>
+template <class Sink>
 __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
                                                WordCache& ltc, const float* act, int t, int i, int p, int& a_i,
                                                int& lt_i, Sink& out, ScAcc& scg_acc_) {
@@ -107,12 +107,12 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
   // Global loads go out kChunk at a time (all issued before the first is used), so a heap
   // copy or an inbox drain waits on memory once per chunk instead of once per entry; the
   // heap size, the stock and the first inbox chunk are requested together up front.
-  // (an inbox kChunk of 8 ran slower.) HCHUNK heap slots per memory round: the kernel
-  // without ledgers takes 16 — all of a deterministic ntom heap's slots at the start of a
-  // step in one round with its size: 256 VGPRs, still two waves per SIMD, 0.7 % faster than
-  // 8 (r03ah; 12: no change) — the ledger one 8 (16 would take it to 264 VGPRs, one wave).
+  // (kChunk = 8 pushed the kernel to 256 VGPRs, one wave per SIMD, and ran slower.)
   constexpr int kChunk = 4;
-  constexpr int kHeapChunk = HCHUNK;
+#ifndef SCG_STAGED_HCHUNK
+#define SCG_STAGED_HCHUNK 8
+#endif
+  constexpr int kHeapChunk = SCG_STAGED_HCHUNK;  // heap slots per memory round
 #ifndef SCG_STAGED_PLAIN
 #define SCG_STAGED_PLAIN 1
 #endif
@@ -196,7 +196,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 // shares. out(o, x) receives the node observation elements (the caller adds the demand and
 // time-to-go ones). Returns the reward. (Staging the node's stocks in LDS as well measured
 // no faster on MI355X: stock accesses are few and cache-resident.)
-template <int MAXD, int HCHUNK = 8, class Sink>
+template <int MAXD, class Sink>
 __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
                                                  const float* act, int t, Sink& out) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
@@ -208,7 +208,7 @@ __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const
   for (int i = 0; i < c.n_nodes; ++i) {
     ScNode& nd = c.nodes[i];
     int a_i = 0, lt_i = 0;
-    for (int p = 0; p < c.P; ++p) sc_staged_heap<HCHUNK>(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out, scg_acc_);
+    for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out, scg_acc_);
     if (!StagedInbox::kClearInAct && !nd.last_level) in.clear(c, i);
     SCG_ACC(7);
     total = np_add(total, sc_node_act<MAXD, StagedInbox, true>(c, g, ltc, dmc, i, act, t, in));
