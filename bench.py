@@ -19,7 +19,10 @@ Timing (rank 0 prints ONE JSON line):
   * the timed region is exactly K steps, bracketed by barrier + synchronize, max over
     ranks; `value` = envs of all ranks x K / that wall time. Nothing inside is stamped
     (stamping the first and last launch cost a K = 20 region 0.3-0.6 us per step,
-    profiles/r02s_stamped_headline_ab.log);
+    profiles/r02s_stamped_headline_ab.log); `headline_split` says what bounds it: the host's
+    enqueue time per step (the loop's wall time up to the final synchronize / K), the wait
+    after it, the same brackets around zero steps (the region's fixed cost) and the GPU
+    time per step of the 100-episode region below;
   * `episodes_timed`: the same over 100 whole episodes (3,500 steps), as SURVEY §8(d)
     asks, with its first and last launch stamped (hipExtLaunchKernel dispatch begin / end):
     that GPU time / 3,500 is `roofline.avg_kernel_us`;
@@ -95,23 +98,57 @@ def profile_tag_key(path):
     return (int(m.group(1)), n)
 
 
-def pmc_traffic(kernel_substr=KERNEL, n_envs=N_ENVS):
-    """HBM bytes per launch of the step kernel from the newest committed PMC summary that
-    has it (profiles/rNN*_pmc_summary.json, tools/pmc_summary.py, separate rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench at 65,536 envs; FETCH_SIZE doubled per
-    MI355X_MICROARCH.md §HBM, calibrated for this repo's access shapes in
-    profiles/r03b_pmc_calib_*.csv). None when absent or for another batch size."""
+# The sources each kernel family is compiled from: a PMC summary counts for a kernel only if
+# it was collected on exactly these bytes (tools/pmc_summary.py records the hash).
+KERNEL_SOURCES = {
+    "bg": ["scg_beergame.hip", "scg_beergame_kernels.h", "scg_bg_levels_1.hip", "scg_bg_levels_2.hip",
+           "scg_bg_levels_3.hip", "scg_bg_levels_4.hip", "scg_common.h", "scg_common.hip", "scg_const.h",
+           "scg_philox.h"],
+    "sc": ["scg_supplychain.hip", "scg_sc_nodes.hip", "scg_supplychain_core.h", "scg_supplychain_nodes.h",
+           "scg_supplychain_staged.h", "scg_supplychain_level.h", "scg_supplychain_args.h", "scg_npscalar.h",
+           "scg_pyheap.h", "scg_common.h", "scg_common.hip", "scg_const.h", "scg_philox.h"],
+}
+
+
+def kernel_sources_hash(family):
+    """sha256 (16 hex digits) of a kernel family's sources and the shared header, in order."""
+    import hashlib
+    h = hashlib.sha256()
+    pkg = os.environ.get("SCG_PKG_ROOT") or os.path.join(REPO, "gym-supplychain_amd")
+    for f in KERNEL_SOURCES[family]:
+        with open(os.path.join(pkg, "csrc", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(REPO, "include", "scgpu.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_lookup(family, workload, kernel_substr):
+    """HBM bytes per launch of `kernel_substr` from the newest committed PMC summary
+    (profiles/rNN*_pmc_summary.json, tools/pmc_summary.py: separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM,
+    calibrated for this repo's access shapes in profiles/r03b_pmc_calib_*.csv) whose
+    recorded workload equals `workload` (every key) and whose source hash is this tree's
+    for `family` — a summary of another workload, or of a kernel since changed, never
+    counts. Returns (bytes, path) or (None, None)."""
     import glob
-    if n_envs != N_ENVS:
-        return None, None
+    src = kernel_sources_hash(family)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), key=profile_tag_key,
                        reverse=True):
         with open(path) as f:
-            traffic = json.load(f).get("traffic", {})
-        for name, t in traffic.items():
+            summ = json.load(f)
+        meta = summ.get("workload") or {}
+        if summ.get("src_hash", {}).get(family) != src or any(meta.get(k) != v for k, v in workload.items()):
+            continue
+        for name, t in summ.get("traffic", {}).items():
             if kernel_substr in name and t.get("hbm_bytes_per_launch"):
                 return t["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
     return None, None
+
+
+def pmc_traffic(kernel_substr=KERNEL, n_envs=N_ENVS):
+    """The bench kernel's HBM bytes per launch at this batch size (pmc_lookup)."""
+    return pmc_lookup("bg", {"bench": "beergame-v0", "n_envs": n_envs}, kernel_substr)
 
 
 # ---- CPU baseline ------------------------------------------------------------------------
@@ -202,19 +239,25 @@ class StepLoop:
                 sync_each()
 
 
-def region(loop, k, world, barrier, sync, stamps=None):
+def region(loop, k, world, barrier, sync, stamps=None, split=None):
     """Time exactly k steps: barrier + sync on both sides. Returns (wall s, GPU ms between
-    the first launch's start and the last one's end, or None without stamps)."""
+    the first launch's start and the last one's end, or None without stamps). With a dict
+    `split`, also its host side: split["enqueue_s"] = the step loop's wall time up to the
+    final synchronize (the host enqueueing k launches), split["drain_s"] = the rest (the
+    synchronize waiting for the GPU, and the closing barrier)."""
     if world > 1:
         barrier()
     sync()
     t0 = time.perf_counter()
     loop.run(k, first=stamps[0] if stamps else None, last=stamps[1] if stamps else None)
+    t1 = time.perf_counter()
     sync()
     if world > 1:
         barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = stamps[2](stamps[0], stamps[1]) if stamps else None
+    if split is not None:
+        split["enqueue_s"], split["drain_s"] = t1 - t0, elapsed - (t1 - t0)
     return elapsed, gpu_ms
 
 
@@ -429,8 +472,11 @@ def run(args, plat):
     gc.disable()  # no collector pass inside a timed region
     try:
         # headline: exactly K steps, unstamped (profiles/r02s_stamped_headline_ab.log)
-        elapsed, _ = region(loop, args.steps, world, barrier, plat.sync)
+        split = {}
+        elapsed, _ = region(loop, args.steps, world, barrier, plat.sync, split=split)
         gather.result()
+        # the fixed cost of a region: the same brackets around zero steps
+        empty, _ = region(loop, 0, world, barrier, plat.sync)
         # 100 whole episodes, from an episode boundary
         loop.run((WEEKS - env.week) % WEEKS)
         k_ep = EPISODES_TIMED * WEEKS
@@ -448,7 +494,8 @@ def run(args, plat):
     for e in ev + [x for pair in iso for x in pair]:
         plat.destroy_event(e)
     env.check_errors()
-    elapsed, ep_elapsed, ep_gpu_ms, iso_ms = max_over_ranks([elapsed, ep_elapsed, ep_gpu_ms, iso_ms], world, device)
+    elapsed, ep_elapsed, ep_gpu_ms, iso_ms, enq_s, drain_s, empty = max_over_ranks(
+        [elapsed, ep_elapsed, ep_gpu_ms, iso_ms, split["enqueue_s"], split["drain_s"], empty], world, device)
     extras = plat.extras() if rank == 0 and world == 1 and not args.no_extras else {}
     if rank != 0:
         return None
@@ -491,6 +538,13 @@ def run(args, plat):
                            "ms_per_step": ep_elapsed * 1e3 / k_ep, "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
                            "frac": ep_bytes / (ep_gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
         "roofline": roof,
+        # what bounds the headline region: the host enqueueing K launches, or the GPU
+        # draining them (max over ranks of each part)
+        "headline_split": {"host_enqueue_us_per_step": enq_s * 1e6 / args.steps,
+                           "drain_after_enqueue_us": drain_s * 1e6,
+                           "empty_region_us": empty * 1e6,
+                           "gpu_kernel_us_per_step": ep_gpu_ms * 1e3 / k_ep,
+                           "bound": "host" if enq_s * 1e6 / args.steps > ep_gpu_ms * 1e3 / k_ep else "gpu"},
         "episode_returns_gathered": gather.gathers,
     }
     if world == 1 and not args.no_cpu_baseline:

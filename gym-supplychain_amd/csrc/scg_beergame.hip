@@ -275,8 +275,7 @@ int scg_bg_prepare(scg_bg_config* cfg) {
     if (cfg->variant != 1) return fail(SCG_ERR_INVALID, "full_table is a BeerGameEnv (variant 1) option");
     int32_t last = T + 1;
     for (int32_t w = 0; w <= T; ++w) last = std::max(last, w + cfg->shipment_delays[w] + 1);
-    R = last + 1;
-    if (R > 127) return fail(SCG_ERR_INVALID, "full_table needs at most 127 rows (this config has %d)", R);
+    R = last + 1;  // <= T + SCG_BG_MAX_DELAY + 2: fits pack_week's slot fields
   }
   // Which arrival weeks have been written, in week order (writes only target later weeks).
   // (a full table also keeps the rows past T: week T + 1 + max delay at most)
@@ -374,7 +373,7 @@ int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t*
     sa.guard = week_guard(cfg->levels, cfg->inv_cost, cfg->backlog_cost);
     sa.err_host = st->error_host;
     for (int l = 0; l < cfg->levels; ++l) sa.init_inv[l] = cfg->initial_inventory[l];
-    uint32_t wpack = pack_week(wk) & 0x3ffffu;
+    uint32_t wpack = pack_week_slab(wk);  // R <= 127 (slab_layout)
     wpack |= (wk.flags & 1) ? SW_TERMINAL : 0u;
     wpack |= (wk.flags & 2) ? SW_AUTORESET : 0u;
     wpack |= st->inventory_costs ? SW_LEDGERS : 0u;

@@ -442,10 +442,20 @@ __device__ __forceinline__ void zero_row(int32_t (&v)[L]) {
 }
 
 // Week plan packed into one dword for the step kernel's preloaded arguments:
-// bits 0-7 read_slot + 1 (0: nothing due), 8-15 write_slot, 16-17 mode, 18-19 flags.
+// bits 0-13 read_slot + 1 (0: nothing due), 14-27 write_slot, 28-29 mode, 30-31 flags
+// (slots < 2^14 > SCG_BG_MAX_WEEKS + SCG_BG_MAX_DELAY + 2, the longest full table).
+constexpr uint32_t kWeekSlotBits = 14, kWeekSlotMask = (1u << kWeekSlotBits) - 1;
+static_assert(SCG_BG_MAX_WEEKS + SCG_BG_MAX_DELAY + 2 < (1 << kWeekSlotBits), "ring slot field too narrow");
 inline uint32_t pack_week(const WeekInfo& wk) {
+  return static_cast<uint32_t>(wk.read_slot + 1) | (static_cast<uint32_t>(wk.write_slot) << kWeekSlotBits) |
+         (static_cast<uint32_t>(wk.mode) << 28) | (static_cast<uint32_t>(wk.flags) << 30);
+}
+
+// The slab kernel's week plan (its ring has at most 127 slots, scg_bg_slab_layout): bits 0-7
+// read_slot + 1, 8-15 write_slot, 16-17 mode; the launcher adds the SW_* option bits and R.
+inline uint32_t pack_week_slab(const WeekInfo& wk) {
   return static_cast<uint32_t>(wk.read_slot + 1) | (static_cast<uint32_t>(wk.write_slot) << 8) |
-         (static_cast<uint32_t>(wk.mode) << 16) | (static_cast<uint32_t>(wk.flags) << 18);
+         (static_cast<uint32_t>(wk.mode) << 16);
 }
 
 // step(action) for one env per lane: every row this launch reads is loaded up front (one
@@ -462,11 +472,11 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
                                                          int32_t* __restrict__ ring_p, uint32_t n32, uint32_t wpack,
                                                          const BgArgs a, const WeekInfo wk) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  const int32_t read_slot = static_cast<int32_t>(wpack & 0xffu) - 1;
-  const int32_t write_slot = static_cast<int32_t>((wpack >> 8) & 0xffu);
-  const int32_t mode = static_cast<int32_t>((wpack >> 16) & 3u);
-  const bool terminal = wpack & (1u << 18);
-  const bool autoreset = wpack & (2u << 18);
+  const int32_t read_slot = static_cast<int32_t>(wpack & kWeekSlotMask) - 1;
+  const int32_t write_slot = static_cast<int32_t>((wpack >> kWeekSlotBits) & kWeekSlotMask);
+  const int32_t mode = static_cast<int32_t>((wpack >> 28) & 3u);
+  const bool terminal = wpack & (1u << 30);
+  const bool autoreset = wpack & (2u << 30);
   const int64_t row = n * L;
   const int64_t stride = static_cast<int64_t>(n32) * L;
   if (n >= static_cast<int64_t>(n32)) return;

@@ -157,7 +157,6 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
     for (int u = 0; u < kAct; ++u)
       if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
     const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
-    constexpr int kStage = 4;  // slots requested with the size (sc_nodes_stage); a longer heap costs a round more
     for (int i = w; i < NN; i += W)
       for (int p = 0; p < P; ++p) {
         const int hp = i * P + p;
@@ -165,31 +164,14 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
         const int64_t r = static_cast<int64_t>(hp) * a.n + n;
         const double st = a.stock[r];
         const int32_t sz = a.size[r];
-        int32_t bt[kStage];
-        double bv[kStage];
-#pragma unroll
-        for (int u = 0; u < kStage; ++u)
-          if (u < H) {
-            bt[u] = a.tk[(static_cast<int64_t>(hp) * H + u) * a.n + n];
-            bv[u] = a.val[(static_cast<int64_t>(hp) * H + u) * a.n + n];
-          }
         stk[hp * 64 + lane] = st;
         hsz[hp * 64 + lane] = sz;
         const HeapView lh = lheap(hp);
-#pragma unroll
-        for (int u = 0; u < kStage; ++u)
-          if (u < H) lh.put(u, HeapEntry{bt[u], bv[u]});
-        for (int j0 = kStage; j0 < sz; j0 += kStage) {  // a heap past kStage entries
-#pragma unroll
-          for (int u = 0; u < kStage; ++u)
-            if (j0 + u < sz) {
-              bt[u] = a.tk[(static_cast<int64_t>(hp) * H + j0 + u) * a.n + n];
-              bv[u] = a.val[(static_cast<int64_t>(hp) * H + j0 + u) * a.n + n];
-            }
-#pragma unroll
-          for (int u = 0; u < kStage; ++u)
-            if (j0 + u < sz) lh.put(j0 + u, HeapEntry{bt[u], bv[u]});
-        }
+        // the heap's first slots are requested with the size (sc_nodes_copy_heap, shared
+        // with the host harness); a longer heap costs a round more
+        sc_nodes_copy_heap(HeapView{a.tk + static_cast<int64_t>(hp) * H * a.n + n,
+                                    a.val + static_cast<int64_t>(hp) * H * a.n + n, a.n},
+                           lh, H, sz);
         bad |= !sc_recv_scan(lh, sz, a.t, recv[hp * 64 + lane]);
       }
     {

@@ -98,26 +98,23 @@ __host__ __device__ inline bool sc_recv_scan(const HeapView& h, int32_t sz, int 
   return ok;
 }
 
-// stage: heap (i, p) from the env's state into `lh` (its size into lsz), and what it
-// releases at t. Loads go out SCG_NODES_STAGE_CHUNK at a time.
+// Heap copy of the stage phase, shared by the kernel (scg_sc_nodes.hip) and the host
+// harness: the slots of heap view gh (HBM) with size sz into lh (LDS), kChunk at a time.
+// The first chunk does not depend on sz (slots past the size are read and stored, never
+// used), so it is requested together with the size — one memory round for a heap of at
+// most kChunk entries — and a longer heap costs a round per further chunk.
 #ifndef SCG_NODES_STAGE_CHUNK
 #define SCG_NODES_STAGE_CHUNK 4
 #endif
-__host__ __device__ inline bool sc_nodes_stage(const ScCtx& c, const ScEnv& g, const HeapView& lh, int32_t& lsz,
-                                               int t, int i, int p, double& recv) {
-  const HeapView gh = sc_heap(c, g, i, p);
-  constexpr int kChunk = SCG_NODES_STAGE_CHUNK;
-  // the first chunk is requested with the size (one memory round instead of two for a heap
-  // of at most kChunk entries; slots past the size are read but not used)
+template <int kChunk = SCG_NODES_STAGE_CHUNK>
+__host__ __device__ __forceinline__ void sc_nodes_copy_heap(const HeapView& gh, const HeapView& lh, int H, int32_t sz) {
   HeapEntry b[kChunk];
-  const int first = c.H < kChunk ? c.H : kChunk;
 #pragma unroll
   for (int u = 0; u < kChunk; ++u)
-    if (u < first) b[u] = gh.get(u);
-  const int32_t sz = sc_size(c, g, i, p);
+    if (u < H) b[u] = gh.get(u);
 #pragma unroll
   for (int u = 0; u < kChunk; ++u)
-    if (u < sz) lh.put(u, b[u]);
+    if (u < H) lh.put(u, b[u]);
   for (int j0 = kChunk; j0 < sz; j0 += kChunk) {
 #pragma unroll
     for (int u = 0; u < kChunk; ++u)
@@ -126,6 +123,14 @@ __host__ __device__ inline bool sc_nodes_stage(const ScCtx& c, const ScEnv& g, c
     for (int u = 0; u < kChunk; ++u)
       if (j0 + u < sz) lh.put(j0 + u, b[u]);
   }
+}
+
+// stage: heap (i, p) from the env's state into `lh` (its size into lsz), and what it
+// releases at t.
+__host__ __device__ inline bool sc_nodes_stage(const ScCtx& c, const ScEnv& g, const HeapView& lh, int32_t& lsz,
+                                               int t, int i, int p, double& recv) {
+  const int32_t sz = sc_size(c, g, i, p);
+  sc_nodes_copy_heap(sc_heap(c, g, i, p), lh, c.H, sz);
   lsz = sz;
   return sc_recv_scan(lh, sz, t, recv);
 }

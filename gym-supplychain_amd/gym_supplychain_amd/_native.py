@@ -38,7 +38,7 @@ SCG_STREAM_BG2_DELAY = 5
 
 BG_MAX_LEVELS = 16
 BG_MAX_WEEKS = 4096
-BG_MAX_DELAY = 63
+BG_MAX_DELAY = 4096
 POISSON_MAX = 256
 BG_ROLLOUT_MAX = 128
 

@@ -27,6 +27,26 @@ def shard_offset(n_per_rank, rank=None):
     return int(rank) * int(n_per_rank)
 
 
+def entropy_seed(seed, seed_group=None):
+    """A 64-bit Philox key: `seed`, or fresh OS entropy for None (RandomState(None) semantics).
+
+    The entropy is this process's own unless `seed_group` names a torch.distributed process
+    group (True: the default group): then the group's rank 0 draws it and every member
+    adopts it, so the shards of one seed=None batch draw what one big batch would
+    (env_offset). That is a collective: every rank of the group must make the same call."""
+    if seed is not None:
+        return int(seed) & 0xFFFFFFFFFFFFFFFF
+    key = [int.from_bytes(os.urandom(8), "little")]
+    if seed_group is not None and seed_group is not False:
+        if not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("seed_group needs an initialised torch.distributed process group")
+        group = None if seed_group is True else seed_group
+        if dist.get_world_size(group) > 1:
+            src = 0 if group is None else dist.get_global_rank(group, 0)
+            dist.broadcast_object_list(key, src=src, group=group)
+    return key[0]
+
+
 def _async_copy(dst, src):
     """dst <- src, async on the current stream. On the GPU one hipMemcpyAsync (device to
     device) through torch's HIP runtime: a torch copy_ costs the host ≈10 µs of dispatch,

@@ -14,7 +14,6 @@ Differences from the reference, all documented in DESIGN.md:
 """
 import ctypes
 import numbers
-import os
 import weakref
 
 import numpy as np
@@ -22,6 +21,7 @@ import torch
 
 from .. import _native as nat
 from .. import spaces
+from ..distributed import entropy_seed
 
 # beergame_env.py:16-23
 STD_LEVELS = 4
@@ -38,18 +38,7 @@ _I32 = (-(2 ** 31), 2 ** 31 - 1)
 ACTION_BOUND = 2 ** 15
 
 
-def _entropy_seed(seed):
-    """A Philox key: `seed`, or fresh OS entropy for None (RandomState(None) semantics).
-
-    Under torch.distributed the entropy is rank 0's, broadcast to every rank, so shards
-    of one seed=None batch keep drawing the demand one big batch would (env_offset)."""
-    if seed is not None:
-        return int(seed) & 0xFFFFFFFFFFFFFFFF
-    key = [int.from_bytes(os.urandom(8), "little")]
-    dist = torch.distributed
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.broadcast_object_list(key, src=0)
-    return key[0]
+_entropy_seed = entropy_seed  # seed=None: this process's entropy unless a seed_group is given
 
 
 def _int32(name, v):
@@ -129,7 +118,8 @@ class BeerGameVecEnv:
             kernel (default; needs N * L % 4 == 0, else separate buffers and the general
             kernel). Both give identical results.
     full_table: keep the reference's whole absolute-week shipment table (beergame_env.py:46-50)
-            instead of the ring of max delay + 1 weeks (`shipment_table()`); at most 127 rows.
+            instead of the ring of max delay + 1 weeks (`shipment_table()`), any row count (past
+            127 rows the state is not one slab: the general step kernel runs).
     Values the reference keeps in int64 are int32 here; a step whose int64 result leaves
     int32 sets a sticky device flag, raised as OverflowError by check_errors() and, one
     episode late (so the step loop never stalls), by the terminal step.
@@ -285,7 +275,7 @@ class BeerGameVecEnv:
         self._cfg_addr, self._st_addr = ctypes.addressof(self._cfg), ctypes.addressof(self._st)
         self._fast_step, self._fast_step_timed = nat.fast.bg_step, nat.fast.bg_step_timed
         self._raw_stream = nat.raw_stream_fn()  # torch's current raw stream, one C call
-        self._ready = {}  # id(actions) -> (weakref, data_ptr, stride) of validated action tensors
+        self._ready = {}  # id(actions) -> (weakref, data_ptr, stride, shape) of validated action tensors
         # gym surface (an extension: the reference leaves both spaces unset, :62-64)
         self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
         # actions: the reference's are unbounded int64 (:121); sampled ones stay within
@@ -305,9 +295,11 @@ class BeerGameVecEnv:
         nat.check(nat.lib.scg_bg_reset(self._cfg_ref, self._st_ref, self._obs.data_ptr(), self._stream()))
         return self._obs
 
-    def seed(self, seed=None):
-        """New Philox key (fresh entropy for None); the next reset() starts episode 0 again."""
-        self._st.seed = _entropy_seed(seed)
+    def seed(self, seed=None, seed_group=None):
+        """New Philox key (fresh entropy for None; with `seed_group`, the group's rank 0
+        entropy — a collective, see distributed.entropy_seed); the next reset() starts
+        episode 0 again."""
+        self._st.seed = _entropy_seed(seed, seed_group)
         self._st.episode, self._st.week = 0, -1
 
     def _actions(self, actions):
@@ -331,16 +323,18 @@ class BeerGameVecEnv:
     def step(self, actions, _events=None):
         # a tensor validated once is recognised by identity and data pointer (the policy's
         # per-week action buffers are reused), skipping the per-call checks
-        # (the stride catches in-place metadata changes that keep the pointer: t_(),
-        # as_strided_(), a shrinking resize_())
+        # (shape and stride catch in-place metadata changes that keep the pointer: t_(),
+        # as_strided_(), resize_() to fewer rows)
         ok = self._ready.get(id(actions))
-        if ok is not None and ok[0]() is actions and ok[1] == actions.data_ptr() and ok[2] == actions.stride():
+        if ok is not None and ok[0]() is actions and ok[1] == actions.data_ptr() and ok[2] == actions.stride() \
+                and ok[3] == actions.shape:
             ptr = ok[1]
         else:
             if self._is_ready(actions):
                 if len(self._ready) >= 64:
                     self._ready.clear()
-                self._ready[id(actions)] = (weakref.ref(actions), actions.data_ptr(), actions.stride())
+                self._ready[id(actions)] = (weakref.ref(actions), actions.data_ptr(), actions.stride(),
+                                         actions.shape)
             else:
                 actions = self._actions(actions)
             ptr = actions.data_ptr()
@@ -505,12 +499,10 @@ class BeerGameEnv(spaces.Env):
     def __init__(self, env_init_info={}, device=None):  # noqa: B006 - reference signature (:11)
         self.DEBUG = False
         cfg = BeerGameConfig(env_init_info)
-        # the reference's whole shipment table (:46-50) when it fits the kernels' 127 rows
-        d = cfg.shipment_delays.astype(np.int64)
-        rows = max(cfg.max_weeks + 1, int((np.arange(d.size) + d + 1).max())) + 1
+        # the reference's whole absolute-week shipment table (:46-50), for any horizon and delays
         self._vec = BeerGameVecEnv(1, env_init_info, demand="fixed", device=device, auto_reset=False,
                                    track_costs=True, track_history=True, track_returns=False, config=cfg,
-                                   full_table=rows <= 127)
+                                   full_table=True)
         cfg = self._vec.config
         self.levels = cfg.levels
         self.inv_cost = cfg.inv_cost
@@ -604,8 +596,6 @@ class BeerGameEnv(spaces.Env):
     def shipments(self):
         """The reference's absolute-week table [rows, L] (:46-52): row w is what arrives in
         week w, past weeks included (the table is never shifted, :73-74)."""
-        if not self._vec.full_table:
-            raise NotImplementedError("this horizon's shipment table has more than the kernels' 127 rows")
         return self._vec.shipment_table()[0].cpu().numpy()
 
     def render(self, mode='human'):  # beergame_env.py:158-175
@@ -617,7 +607,7 @@ class BeerGameEnv(spaces.Env):
         print('Orders placed:\t', self.orders_placed)
         if self.week is not None and self.week < self.max_weeks:
             print('Next customer demand:\t', self.customer_demand[self.week])
-        if self._vec.full_table and self.week is not None:
+        if self.week is not None:
             table = self.shipments
             print('Next shipments:\t', [(i, list(table[i])) for i in range(self.week + 1, self.week + 6)
                                         if i < len(table)])
@@ -703,7 +693,7 @@ class BeerGame2VecEnv(BeerGameVecEnv):
     def __init__(self, n_envs, max_stock=100, max_order=30, weeks=35, levels=4, customer_demand=None,
                  initial_inventory=(12, 12, 12, 12), inv_cost=1, backlog_cost=2, exceeded_capacity_penalty=100,
                  shipment_delays=2, initial_shipment=4, initial_orders=4, seed=None, device=None, env_offset=0,
-                 auto_reset=True, track_costs=True, track_history=False, track_returns=True):
+                 auto_reset=True, track_costs=True, track_history=False, track_returns=True, seed_group=None):
         if customer_demand is None:
             customer_demand = [4] * 4 + [8] * 31
         cfg = _Bg2Config(max_stock, max_order, weeks, levels, customer_demand, list(initial_inventory), inv_cost,
@@ -712,8 +702,9 @@ class BeerGame2VecEnv(BeerGameVecEnv):
         if cfg.delay_range:
             fields.update(stochastic_delays=1, delay_lo=cfg.delay_range[0], delay_hi=cfg.delay_range[1])
         demand = ("uniform",) + cfg.demand_range if cfg.demand_range else "fixed"
-        # seed=None: fresh entropy, as the reference's RandomState(None) (beergame2_env.py:58)
-        super().__init__(n_envs, None, demand=demand, seed=_entropy_seed(seed), device=device,
+        # seed=None: fresh entropy, as the reference's RandomState(None) (beergame2_env.py:58);
+        # shards of one batch share rank 0's only when asked (seed_group, a collective)
+        super().__init__(n_envs, None, demand=demand, seed=_entropy_seed(seed, seed_group), device=device,
                          env_offset=env_offset, auto_reset=auto_reset, track_costs=track_costs,
                          track_history=track_history, track_returns=track_returns, config=cfg, variant_fields=fields)
         self.max_stock, self.max_order = cfg.max_stock, cfg.max_order

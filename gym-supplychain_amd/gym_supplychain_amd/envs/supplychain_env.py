@@ -20,7 +20,6 @@ Differences from the reference:
     drop-in env returns it with the reference's per-entry NumPy types.
 """
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -28,6 +27,7 @@ import torch
 from .. import _native as nat
 from .. import spaces
 from . import demand
+from ..distributed import entropy_seed
 
 _MAXP = nat.SC_MAX_PRODUCTS
 _MAXD = nat.SC_MAX_DESTS
@@ -198,10 +198,9 @@ class SupplyChainSpec:
         return table
 
 
-def _default_seed(seed):
-    if seed is None:  # RandomState(None) draws fresh entropy (:564); so do we
-        return int.from_bytes(os.urandom(8), "little")
-    return int(seed) & 0xFFFFFFFFFFFFFFFF
+def _default_seed(seed, seed_group=None):
+    # RandomState(None) draws fresh entropy (:564); so do we (distributed.entropy_seed)
+    return entropy_seed(seed, seed_group)
 
 
 class SupplyChainVecEnv:
@@ -236,7 +235,7 @@ class SupplyChainVecEnv:
 
     def __init__(self, n_envs, nodes_info=None, spec=None, seed=0, device=None, env_offset=0, auto_reset=True,
                  obs_dtype=torch.float32, track_returns=True, demand_table=None, leadtime_table=None, kernel="auto",
-                 **kwargs):
+                 seed_group=None, **kwargs):
         if spec is None:
             if nodes_info is None:
                 raise ValueError("pass nodes_info (+ SupplyChainEnv keywords) or a SupplyChainSpec")
@@ -338,7 +337,7 @@ class SupplyChainVecEnv:
         self._done_false = torch.zeros(n_envs, dtype=torch.bool, device=dev)
         self._done_true = torch.ones(n_envs, dtype=torch.bool, device=dev)
         s = nat.ScState()
-        s.n_envs, s.env_offset, s.seed = n_envs, int(env_offset), _default_seed(seed)
+        s.n_envs, s.env_offset, s.seed = n_envs, int(env_offset), _default_seed(seed, seed_group)
         s.episode, s.time_step = 0, -1
         s.stock, s.heap_tk, s.heap_val = self._stock.data_ptr(), self._heap_tk.data_ptr(), self._heap_val.data_ptr()
         s.heap_size, s.error_flags = self._heap_size.data_ptr(), self._err.data_ptr()
@@ -388,9 +387,10 @@ class SupplyChainVecEnv:
     def _stream(self):
         return nat.raw_stream(self._dev_index)
 
-    def seed(self, seed=None):
-        """New Philox key and episode counter 0 (the reference re-creates its RandomState, :811-813)."""
-        self._st.seed = _default_seed(seed)
+    def seed(self, seed=None, seed_group=None):
+        """New Philox key and episode counter 0 (the reference re-creates its RandomState, :811-813);
+        seed=None with `seed_group`: the group's rank 0 entropy (a collective)."""
+        self._st.seed = _default_seed(seed, seed_group)
         self._st.episode = 0
         self._st.time_step = -1
 

@@ -45,7 +45,7 @@ extern "C" {
 
 #define SCG_BG_MAX_LEVELS 16   /* template instantiations of the step kernel        */
 #define SCG_BG_MAX_WEEKS 4096  /* episode horizon (len(customer_demand), :37)        */
-#define SCG_BG_MAX_DELAY 63    /* shipment delay bound: ring slots R = max delay + 1 */
+#define SCG_BG_MAX_DELAY 4096  /* shipment delay bound: ring slots R = max delay + 1 */
 #define SCG_POISSON_MAX 256    /* CDF threshold table entries                        */
 #define SCG_BG_ROLLOUT_MAX 128 /* weeks per rollout launch (host loops beyond)       */
 
@@ -109,7 +109,8 @@ typedef struct scg_bg_config {
    * horizon are stored as the reference stores them. Rows are not cleared between
    * episodes: a row not yet scheduled in the current episode holds a stale value (the
    * reference's is 0; scg_bg_prepare's plan says which rows are scheduled by each week).
-   * Needs ring_slots <= 127. */
+   * Any row count (T + max delay + 2 at most); the state slab, and so the slab step kernel,
+   * takes ring_slots <= 127, a longer table separate buffers and the general step kernel. */
   int32_t full_table;
 } scg_bg_config;
 

@@ -8,7 +8,7 @@ same draws the HIP kernel makes on device. Nothing is written under /root/refere
 (bytecode writing is disabled). On a machine without /root/reference this script exits
 cleanly without touching tests/golden/.
 
-    python oracle/gen_golden.py            # rewrites tests/golden/beergame_*.npz
+    python oracle/gen_golden.py [case ...] # rewrites tests/golden/beergame_*.npz (or those cases)
 """
 import os
 import sys
@@ -50,6 +50,10 @@ CASES = {
     # 1-level chain edge case (incoming[1:] / [:-1] slices are empty)
     "levels1": dict(info=dict(levels=1, initial_inventory=[5]), n_envs=8, weeks=12, lam=3.0, seed=9,
                     episode=0, act_range=(0, 5), act_seed=5),
+    # a 150-week horizon with delays up to 70: the reference's table has 222
+    # rows (:46-50), past the state slab's 127, and rows past the horizon are written
+    "long_delay70": dict(info=dict(), delays=("pattern", [70, 3, 0, 12, 70, 1, 45, 2, 0, 70, 6, 33]),
+                         n_envs=4, weeks=150, lam=8.0, seed=31, episode=0, act_range=(-3, 12), act_seed=6),
 }
 
 
@@ -136,7 +140,10 @@ def main():
     sys.path.insert(0, REFERENCE)
     sys.path.insert(0, os.path.join(HERE, "refharness"))
     os.makedirs(OUT, exist_ok=True)
+    only = set(sys.argv[1:])  # case names to (re)write; all by default
     for name, spec in CASES.items():
+        if only and name not in only:
+            continue
         info, demand, actions, thr = case_inputs(name, spec)
         rec = run_reference(info, demand, actions)
         T, N, L = actions.shape

@@ -5,11 +5,12 @@ batch env (oracle.beergame.BeerGameOracle per env, the device's Philox demand pe
 id). Rank 0's gathered returns must equal a 1-rank run over the concatenated shards. The
 last test runs bench.run() itself — the whole flow the driver's 8-GPU launch takes: warm-up,
 dry region, headline region, 100 stamped episodes, isolated launches, max over ranks and
-rank 0's JSON line — on two gloo ranks with that stand-in as the platform."""
+rank 0's JSON line — on 2, 4 and 8 gloo ranks with that stand-in as the platform."""
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -128,8 +129,8 @@ class CpuPlatform:
         self._base = bench.Platform()
 
     def make_env(self, n_envs, env_offset):
-        env = StampedBatch(n_envs, env_offset)
-        return env
+        self.env = StampedBatch(n_envs, env_offset)
+        return self.env
 
     def week_actions(self, env, n_envs):
         return _week_actions(n_envs, env.env_offset)
@@ -182,43 +183,74 @@ def _run_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import bench
+        import gym_supplychain_amd.distributed as gd
+        seen = {"local": []}
+
+        class RecordingGather(gd.EpisodeReturnGather):  # what bench.run() hands to the gather
+            def __init__(self, *a, **k):
+                super().__init__(*a, **k)
+                seen["gather"] = self
+
+            def on_episode_end(self, final_return):
+                seen["local"].append(final_return.clone())
+                super().on_episode_end(final_return)
+
+        gd.EpisodeReturnGather = RecordingGather
+        plat = CpuPlatform(world, rank)
         args = bench.parse_args(["--gpus", str(world), "--envs", "2", "--steps", "20", "--warmup", "5",
                                  "--kernel-samples", "35", "--no-extras", "--no-cpu-baseline"])
-        line = bench.run(args, CpuPlatform(world, rank))
-        q.put((rank, line))
+        line = bench.run(args, plat)
+        gathered = seen["gather"].result().tolist()   # the last episode end's all-gather
+        q.put((rank, dict(line=line, env_offset=plat.env.env_offset, gathered=gathered,
+                          local=seen["local"][-1].tolist(), ends=len(seen["local"]))))
     finally:
         dist.destroy_process_group()
 
 
-def test_bench_run_on_two_ranks_emits_the_rank0_line():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_run_emits_the_rank0_line(world):
+    """bench.run() on `world` gloo ranks (the 8-rank case is the driver's 8-GPU launch shape):
+    global shard offsets, every rank's all-gather holding the shards in rank order, and rank
+    0's line (n_gpus, whole-job value)."""
     import json
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_run_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[1] is None                                   # only rank 0 prints
-    line = json.loads(json.dumps(res[0]))                   # the line is plain JSON
+    n = 2
+    for r in range(world):
+        assert res[r]["env_offset"] == r * n                  # rank r owns global ids [r*n, (r+1)*n)
+        assert res[r]["ends"] == res[0]["ends"]
+        if r:
+            assert res[r]["line"] is None                     # only rank 0 prints
+    want = [x for r in range(world) for x in res[r]["local"]]  # the shards in rank order
+    for r in range(world):
+        assert res[r]["gathered"] == want
+    line = json.loads(json.dumps(res[0]["line"]))             # the line is plain JSON
     assert line["metric"] == "env-steps/sec at 65536 envs/GPU, beergame-v0; 1/2/4/8 MI355X"
-    assert line["n_gpus"] == 2 and line["steps"] == 20 and line["warmup"] == 5
+    assert line["n_gpus"] == world and line["steps"] == 20 and line["warmup"] == 5
     assert line["scaling"] == "weak" and line["higher_is_better"] is True and line["unit"] == "env-steps/s"
     cfg = line["config"]
-    assert cfg["episode_return_allgather"] is True and cfg["parallelism"] == "env-shard x2"
-    assert cfg["n_envs_per_gpu"] == 2
-    # whole-job throughput: envs of both ranks x K over the max-over-ranks wall time
-    assert abs(line["value"] - 2 * 2 * 20 / (line["ms_per_step"] * 20 / 1e3)) < 1e-6 * line["value"]
+    assert cfg["episode_return_allgather"] is True and cfg["parallelism"] == f"env-shard x{world}"
+    assert cfg["n_envs_per_gpu"] == n
+    # whole-job throughput: envs of every rank x K over the max-over-ranks wall time
+    assert abs(line["value"] - world * n * 20 / (line["ms_per_step"] * 20 / 1e3)) < 1e-6 * line["value"]
     assert line["warmup_steps_run"] == 35 + 20                # one whole episode, then the dry region
     ep = line["episodes_timed"]
     assert ep["episodes"] == 100 and ep["steps"] == 3500
     roof = line["roofline"]
     assert roof["launches_timed"] == 3500 and roof["isolated_launches"] == 35
     assert roof["bytes_per_launch"] > 0 and "measured_peak" not in roof and "cpu_baseline" not in line
+    split = line["headline_split"]
+    assert split["host_enqueue_us_per_step"] > 0 and split["empty_region_us"] >= 0
+    assert split["bound"] in ("host", "gpu")
     # every episode end of the run was all-gathered: warm-up 35 + dry 20 + headline 20 +
     # the walk to the boundary + 3,500 + 35 isolated steps
     total = 35 + 20 + 20 + (35 - (35 + 20 + 20) % 35) % 35 + 3500 + 35
-    assert line["episode_returns_gathered"] == total // 35
+    assert line["episode_returns_gathered"] == total // 35 == res[0]["ends"]

@@ -50,3 +50,49 @@ def test_episode_return_allgather_gloo():
         for ep, o in enumerate(outs):
             want = [i + 1000 * r + 100000 * ep for r in range(world) for i in range(n)]
             assert o == want
+
+
+def _seed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gym_supplychain_amd.distributed import entropy_seed
+        out = {"explicit": entropy_seed(2 ** 64 + 5)}
+        out["synced"] = entropy_seed(None, seed_group=True)      # a collective: every rank calls it
+        out["local"] = [entropy_seed(None) for _ in range(4)]    # no collective: rank-local entropy
+        if rank == 0:                                            # one rank alone (a rank-0 eval env)
+            out["rank0_only"] = entropy_seed(None)
+        dist.barrier()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_entropy_seed_is_local_unless_a_group_is_given():
+    """seed=None draws this process's entropy without any collective (so one rank may build
+    an env alone without hanging); with seed_group every rank of the group takes
+    rank 0's, so the shards of one batch keep drawing one big batch's demand."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0]["explicit"] == res[1]["explicit"] == 5
+    assert res[0]["synced"] == res[1]["synced"]
+    assert res[0]["local"] != res[1]["local"]
+    assert "rank0_only" in res[0] and "rank0_only" not in res[1]
+
+
+def test_entropy_seed_group_needs_a_process_group():
+    from gym_supplychain_amd.distributed import entropy_seed
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    with pytest.raises(RuntimeError):
+        entropy_seed(None, seed_group=True)
+    assert entropy_seed(7, seed_group=True) == 7

@@ -268,6 +268,7 @@ def test_sharding_is_invariant():
 
 def test_errors():
     from gym_supplychain_amd import BeerGameVecEnv
+    from gym_supplychain_amd import _native as nat
     env = BeerGameVecEnv(8, {}, device=DEV)
     with pytest.raises(RuntimeError):
         env.step(torch.zeros((8, 4), dtype=torch.int32, device=DEV))
@@ -277,7 +278,7 @@ def test_errors():
     with pytest.raises(ValueError):
         BeerGameVecEnv(8, {}, demand="poisson", poisson_lambda=-1.0, device=DEV)
     with pytest.raises(ValueError):
-        BeerGameVecEnv(8, {"shipment_delays": [99] * 35}, device=DEV)
+        BeerGameVecEnv(8, {"shipment_delays": [nat.BG_MAX_DELAY + 1] * 35}, device=DEV)
 
 
 def test_timed_step_matches_and_stamps_kernel():
@@ -505,6 +506,14 @@ def test_action_cache_sees_metadata_changes():
     env.step(a.contiguous())
     want = env.orders_placed.clone()
     assert torch.equal(got, want) and not torch.equal(got, ref)
+    # resize_ to fewer rows keeps the pointer and the stride (L, 1): the shape check refuses it
+    b = torch.arange(N * L, dtype=torch.int32, device=DEV).view(N, L)
+    env.reset()
+    env.step(b)
+    b.resize_((N - 1, L))
+    env.reset()
+    with pytest.raises(ValueError):
+        env.step(b)
 
 
 def test_overflow_reported_at_next_terminal_step_and_by_other_kernels():

@@ -82,23 +82,13 @@ def cpu_baseline(name, budget=1.5, max_procs=16):
                       f"oracle.supplychain.SupplyChainOracle; {steps} env-steps"}
 
 
-def pmc_traffic(symbol, n_envs, name):
-    """HBM bytes per launch of `symbol` from the newest committed PMC summary that has it
-    (profiles/r*_pmc_summary.json, e.g. tools/gpu_sc_traffic.sh at the default sizes with
-    the auto kernels; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM). None when absent or
-    for another batch size."""
-    import glob
-    if n_envs != SCENARIOS[name]["n_envs"]:
-        return None, None
-    from bench import profile_tag_key
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), key=profile_tag_key,
-                       reverse=True):
-        with open(path) as f:
-            traffic = json.load(f).get("traffic", {})
-        for k, t in traffic.items():
-            if symbol.split("::")[-1] in k and t.get("hbm_bytes_per_launch"):
-                return t["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
-    return None, None
+def pmc_traffic(symbol, n_envs, name, kernel, build_info):
+    """HBM bytes per launch of `symbol` from the newest committed PMC summary of exactly this
+    workload — scenario, batch size, kernel choice and ledger mode — collected on this
+    tree's SupplyChain sources (bench.pmc_lookup; tools/gpu_sc_traffic.sh writes them)."""
+    from bench import pmc_lookup
+    workload = {"bench": "bench_sc", "scenario": name, "n_envs": n_envs, "kernel": kernel, "build_info": bool(build_info)}
+    return pmc_lookup("sc", workload, symbol.split("::")[-1])
 
 
 def run(name, steps, warmup, n_envs, cpu, kernel="auto", build_info=False):
@@ -129,7 +119,7 @@ def run(name, steps, warmup, n_envs, cpu, kernel="auto", build_info=False):
     kern_s = sum(s.elapsed_time(e) for s, e in ev) / 1e3 / steps
     bpe = sc["bytes_per_env_step"]
     achieved = bpe * N / kern_s / 1e9
-    traffic, traffic_src = pmc_traffic(env.kernel_symbol, N, name)
+    traffic, traffic_src = pmc_traffic(env.kernel_symbol, N, name, kernel, build_info)
     line = {"metric": f"env-steps/sec, {sc['env_id']} {sc['kwargs'] or ''} x{N} envs on 1 MI355X",
             "value": N * steps / wall, "unit": "env-steps/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
             "ms_per_step": wall * 1e3 / steps, "higher_is_better": True, "dtype": "f32 actions/obs, f64 state",
@@ -151,7 +141,7 @@ def run(name, steps, warmup, n_envs, cpu, kernel="auto", build_info=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--scenario", default="both", choices=["2perstage", "2perstage_mp", "ntom", "both"])
+    ap.add_argument("--scenario", default="both", choices=["2perstage", "2perstage_mp", "ntom", "both", "all"])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=0)
@@ -159,7 +149,8 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "staged", "nodes", "all", "both"])
     ap.add_argument("--build-info", action="store_true", help="keep the build_info ledgers (info['sc_episode'])")
     a = ap.parse_args()
-    for name in (["2perstage", "ntom"] if a.scenario == "both" else [a.scenario]):
+    names = {"both": ["2perstage", "ntom"], "all": ["2perstage", "2perstage_mp", "ntom"]}.get(a.scenario, [a.scenario])
+    for name in names:
         kernels = [a.kernel]
         if a.kernel in ("all", "both"):  # the node-parallel kernel only takes chains whose block fits LDS
             kernels = ["lane", "level", "staged"] + (["nodes"] if name != "ntom" else [])

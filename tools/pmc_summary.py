@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc CSVs (tools/gpu_pmc.sh) per kernel.
 
-    python tools/pmc_summary.py gpurun_out/pmc_r01 > profiles/r01_pmc_summary.json
+    python tools/pmc_summary.py gpurun_out/pmc_r01 --meta bench=beergame-v0 n_envs=65536 --family bg \
+        > profiles/r01_pmc_summary.json
 
 For every pass directory, averages each counter per kernel name over its dispatches.
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are
@@ -25,7 +26,7 @@ def load(pass_dir):
             for k, d in acc.items()}
 
 
-def main(root):
+def main(root, meta=None, families=()):
     out = {}
     for d in sorted(glob.glob(os.path.join(root, "*"))):
         if os.path.isdir(d):
@@ -40,9 +41,36 @@ def main(root):
                           "read_bytes_corrected": None if f is None else 2 * f * 1024,
                           "write_bytes": None if w is None else w * 1024,
                           "hbm_bytes_per_launch": None if (f is None or w is None) else (2 * f + w) * 1024}
-    json.dump({"passes": out, "traffic": traffic}, sys.stdout, indent=1, sort_keys=True)
+    summ = {"passes": out, "traffic": traffic}
+    if meta:
+        summ["workload"] = meta
+    # the kernel sources the passes ran: written by the GPU script next to the passes
+    # (src_hash_<family>.txt), else this tree's (bench.kernel_sources_hash)
+    if families:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import kernel_sources_hash
+        summ["src_hash"] = {}
+        for fam in families:
+            p = os.path.join(root, f"src_hash_{fam}.txt")
+            summ["src_hash"][fam] = open(p).read().strip() if os.path.exists(p) else kernel_sources_hash(fam)
+    json.dump(summ, sys.stdout, indent=1, sort_keys=True)
     print()
 
 
+def _value(v):
+    if v in ("true", "false"):
+        return v == "true"
+    try:
+        return int(v)
+    except ValueError:
+        return v
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--meta", nargs="*", default=[], help="workload key=value pairs (bench.pmc_lookup matches them)")
+    ap.add_argument("--family", nargs="*", default=[], help="kernel families whose source hash to record (bg, sc)")
+    a = ap.parse_args()
+    main(a.root, {k: _value(v) for k, v in (x.split("=", 1) for x in a.meta)}, a.family)
