@@ -10,7 +10,9 @@
 // only when they are equal compare the amounts with NumPy scalar semantics.
 //
 // Layout: entry j of a heap lives at index j*stride of `tk` (time << 3 | NumPy kind) and
-// `val` (amount as double), so env-major strided heaps of many envs can share arrays.
+// `val` (amount as double), so env-major strided heaps of many envs can share arrays. The
+// functions below take any view type with get / put / time_at (HeapView here; the staged
+// kernel's byte-packed HeapView8 in scg_supplychain_staged.h).
 #pragma once
 
 #include "scg_npscalar.h"
@@ -64,8 +66,8 @@ struct HeapView {
 // entries being moved in registers the same way, so each heap slot is read once per sift
 // level (the heap is in LDS in every kernel but the lane one on HBM heaps: these reads are
 // a chain of dependent latencies).
-template <bool kPlain = false>
-__host__ __device__ inline void py_siftdown_item(const HeapView& h, int startpos, int pos, const HeapEntry& item) {
+template <bool kPlain = false, class HV>
+__host__ __device__ inline void py_siftdown_item(const HV& h, int startpos, int pos, const HeapEntry& item) {
   while (pos > startpos) {
     const int parentpos = (pos - 1) >> 1;
     const HeapEntry parent = h.get(parentpos);
@@ -79,13 +81,15 @@ __host__ __device__ inline void py_siftdown_item(const HeapView& h, int startpos
   h.put(pos, item);
 }
 
-__host__ __device__ inline void py_siftdown(const HeapView& h, int startpos, int pos) {
+template <class HV>
+__host__ __device__ inline void py_siftdown(const HV& h, int startpos, int pos) {
   py_siftdown_item(h, startpos, pos, h.get(pos));
 }
 
 // heapq._siftup(heap, pos) for `item` standing at pos: move the smaller child up to a leaf,
 // then sift the item down from there (CPython's bottom-up variant).
-__host__ __device__ inline void py_siftup_item(const HeapView& h, int size, int pos, const HeapEntry& item) {
+template <class HV>
+__host__ __device__ inline void py_siftup_item(const HV& h, int size, int pos, const HeapEntry& item) {
   const int startpos = pos;
   int childpos = 2 * pos + 1;
   while (childpos < size) {
@@ -105,7 +109,8 @@ __host__ __device__ inline void py_siftup_item(const HeapView& h, int size, int 
   py_siftdown_item(h, startpos, pos, item);
 }
 
-__host__ __device__ inline void py_siftup(const HeapView& h, int size, int pos) {
+template <class HV>
+__host__ __device__ inline void py_siftup(const HV& h, int size, int pos) {
   py_siftup_item(h, size, pos, h.get(pos));
 }
 
@@ -114,8 +119,8 @@ __host__ __device__ inline void py_siftup(const HeapView& h, int size, int pos) 
 // heap is not empty afterwards), so a loop of pops reads no slot twice: the bottom-up
 // sift's first move puts the smaller child at the root, and the re-seated last entry lands
 // there only if it climbs all the way back.
-template <bool kPlain = false>
-__host__ __device__ inline HeapEntry py_heappop_root(const HeapView& h, int32_t& size, HeapEntry& root) {
+template <bool kPlain = false, class HV>
+__host__ __device__ inline HeapEntry py_heappop_root(const HV& h, int32_t& size, HeapEntry& root) {
   --size;
   const HeapEntry last = h.get(size);
   const HeapEntry ret = root;
@@ -154,7 +159,8 @@ __host__ __device__ inline HeapEntry py_heappop_root(const HeapView& h, int32_t&
 }
 
 // heapq.heappush. Returns false (and pushes nothing) when the heap is full.
-__host__ __device__ inline bool py_heappush(const HeapView& h, int32_t& size, int cap, const HeapEntry& e) {
+template <class HV>
+__host__ __device__ inline bool py_heappush(const HV& h, int32_t& size, int cap, const HeapEntry& e) {
   if (size >= cap) return false;
   ++size;
   py_siftdown_item(h, 0, size - 1, e);  // heap.append(e); _siftdown(heap, 0, len - 1)
@@ -162,7 +168,8 @@ __host__ __device__ inline bool py_heappush(const HeapView& h, int32_t& size, in
 }
 
 // heapq.heappop on a non-empty heap.
-__host__ __device__ inline HeapEntry py_heappop(const HeapView& h, int32_t& size) {
+template <class HV>
+__host__ __device__ inline HeapEntry py_heappop(const HV& h, int32_t& size) {
   --size;
   const HeapEntry last = h.get(size);
   if (size > 0) {

@@ -221,15 +221,15 @@ void sc_step_staged_kernel(const ScArgs a) {
   if (n >= a.n) return;
   const ScCtx& c = a.c;
   double* lval = reinterpret_cast<double*>(smem);
-  const int slots = c.H > MAXD ? c.H : MAXD;  // sc_staged_lds_bytes
-  int32_t* ltk = reinterpret_cast<int32_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
+  const int slots = c.H > MAXD ? c.H : MAXD;  // sc_staged_lds_bytes: 9 bytes per slot and lane
+  uint8_t* ltk = reinterpret_cast<uint8_t*>(lval + static_cast<int64_t>(slots) * kScBlock);
   ScEnv g = env_view(a, n, a.episode);
   if constexpr (!LED) {
     g.led_v = nullptr;
     g.led_k = nullptr;
   }
-  const HeapView lh{ltk + lane, lval + lane, kScBlock};
-  const StagedInbox in{a.inbox_tk + n, a.inbox_val + n, a.n, lh};
+  const HeapView8 lh{ltk + lane, lval + lane, kScBlock};
+  const StagedInbox in{a.inbox_tk + n, a.inbox_val + n, a.n, lh, a.t};
   const bool terminal = a.flags & 1;
   const bool autoreset = a.flags & 2;
   // node observations go to obs, or to the terminal observation when the env resets now
@@ -549,7 +549,7 @@ int sc_lds_epb(int64_t n) {
 }
 // Staged kernel: one heap per lane, or the split's scratch (sc_split_scratch) when wider.
 size_t sc_staged_lds_bytes(const scg_sc_config* cfg) {
-  return kScBlock * static_cast<size_t>(std::max(cfg->heap_capacity, sc_maxd_bucket(cfg->max_dests))) * 12;
+  return kScBlock * static_cast<size_t>(std::max(cfg->heap_capacity, sc_maxd_bucket(cfg->max_dests))) * 9;
 }
 
 // The staged kernel's inbox (scg_supplychain_staged.h): every shipment must go to a later
@@ -712,7 +712,13 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
     if (entries >= 0 && (2 * lds <= sc_nodes_lds_max() || (lds <= sc_nodes_lds_max() && sc_lds_bytes(cfg) > kScLdsMax)))
       want = SCG_SC_KERNEL_NODES;
   }
-  if (want == SCG_SC_KERNEL_AUTO && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
+  // the staged kernel's byte-packed entries hold times up to kStagedMaxRel after the step's
+  // (scg_supplychain_staged.h): lead times, and the initial pipeline at times 1..k
+  int rel_max = std::max(cfg->avg_leadtime, cfg->max_leadtime);
+  for (int i = 0; i < NN; ++i)
+    for (int p = 0; p < P; ++p) rel_max = std::max(rel_max, nodes[i].n_init[p]);
+  const bool staged_ok = rel_max <= kStagedMaxRel;
+  if (want == SCG_SC_KERNEL_AUTO && staged_ok && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
     std::vector<scg_sc_node> probe(nodes, nodes + NN);
     if (sc_inbox_layout(cfg, probe.data()) >= 0) want = SCG_SC_KERNEL_STAGED;
   }
@@ -738,6 +744,8 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
       return fail(SCG_ERR_INVALID, "the staged kernel needs every shipment to go to a later node, once per list");
     if (sc_staged_lds_bytes(cfg) > kScLdsMax)
       return fail(SCG_ERR_INVALID, "one node's heaps (%d products x %d slots) exceed the staged kernel's LDS", P, H);
+    if (!staged_ok)
+      return fail(SCG_ERR_INVALID, "the staged kernel holds lead times up to %d (this chain: %d)", kStagedMaxRel, rel_max);
     cfg->inbox_size = entries;
     cfg->kernel = SCG_SC_KERNEL_STAGED;
     cfg->layout = SCG_SC_LAYOUT_ENV_FASTEST;

@@ -23,7 +23,7 @@ struct ScArgs {
   double* ep_ret;
   double* final_ret;
   int32_t* err;
-  int32_t* inbox_tk;  // staged kernel: shipment inbox [inbox_size][N]
+  uint8_t* inbox_tk;  // staged kernel: shipment inbox [inbox_size][N] (scg_supplychain_staged.h)
   double* inbox_val;
   double* led_v;     // build_info ledgers [2*8*P][N] (lane kernels) or null
   int32_t* led_k;

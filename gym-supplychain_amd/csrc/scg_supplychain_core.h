@@ -478,8 +478,8 @@ __host__ __device__ __forceinline__ void sc_ship_vals(const float* raw, int base
 }
 
 // receive (:220-228) for one heap: pop every entry due now, summed in a float64 array
-template <bool kPlain = false>
-__host__ __device__ __forceinline__ double sc_receive(const HeapView& h, int32_t& sz, int t) {
+template <bool kPlain = false, class HV>
+__host__ __device__ __forceinline__ double sc_receive(const HV& h, int32_t& sz, int t) {
   double recv = 0.0;
   // the root travels in registers from pop to pop (py_heappop_root): no slot read twice
   if (sz == 0) return recv;
@@ -702,8 +702,8 @@ inline constexpr bool kNoVisit<NoVisit> = true;
 
 // node i, product p: avg_leadtime in-transit bins over heap h of size sz (:445-461). The
 // walk reads every entry once, in storage order; visit(k, entry) sees each of them.
-template <class Sink, class Visit = NoVisit>
-__host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HeapView& h, int32_t sz, int t, int i, int p,
+template <class Sink, class Visit = NoVisit, class HV>
+__host__ __device__ inline void sc_observe_bins(const ScCtx& c, const HV& h, int32_t sz, int t, int i, int p,
                                                 Sink& out, const Visit& visit = Visit()) {
   ScNode& nd = c.nodes[i];
   const int nb = c.avg_lt;

@@ -22,29 +22,49 @@
 // Heap storage order, float rounding and the lead-time cursor are the reference's (the
 // pushes into a heap happen in the same order, before the same pops). The inbox is a
 // per-env HBM array laid out by scg_sc_prepare (scg_sc_node in_base/in_deg/in_slot).
+//
+// Byte-packed entries: inside the step, every time a staged heap or the inbox holds lies in
+// [t, t + max_leadtime], so both keep an entry's time RELATIVE to t with its NumPy kind in
+// one byte (rel << 3 | kind; max_leadtime <= kStagedMaxRel) next to its float64 amount:
+// 9 bytes instead of 12, in LDS (the staged heap: 64 lanes x slots x 9 B, which lets 11
+// waves share a CU instead of 8) and in HBM (the inbox: a quarter less traffic). Relative
+// times order, compare and bin exactly as the absolute ones (the step's own time is 0);
+// they are made absolute again only where a heap goes back to HBM.
 #pragma once
 
 #include "scg_supplychain_core.h"
 
 namespace scg {
 
-__host__ __device__ __forceinline__ int32_t sc_f2i(float f) {
-  int32_t i;
-  __builtin_memcpy(&i, &f, sizeof(i));
-  return i;
-}
-__host__ __device__ __forceinline__ float sc_i2f(int32_t i) {
-  float f;
-  __builtin_memcpy(&f, &i, sizeof(f));
-  return f;
-}
+// Largest relative time a byte-packed entry holds (5 bits); 0xFF (relative time 31, kind 7)
+// marks an empty inbox entry. scg_sc_prepare keeps chains with max_leadtime > 30 off this
+// kernel.
+constexpr int kStagedMaxRel = 30;
+constexpr uint8_t kStagedNone = 0xFF;
+
+// A heap of byte-packed entries (rel << 3 | kind, then the amount), entry j at [j * stride].
+struct HeapView8 {
+  uint8_t* tk;
+  double* val;
+  int64_t stride;
+
+  __host__ __device__ __forceinline__ HeapEntry get(int i) const {
+    return HeapEntry{static_cast<int32_t>(tk[i * stride]), val[i * stride]};
+  }
+  __host__ __device__ __forceinline__ void put(int i, const HeapEntry& e) const {
+    tk[i * stride] = static_cast<uint8_t>(e.tk);
+    val[i * stride] = e.v;
+  }
+  __host__ __device__ __forceinline__ int32_t time_at(int i) const { return he_time(tk[i * stride]); }
+};
 
 // Shipments into the destinations' inbox entries; entry q of this env at [q * stride].
 struct StagedInbox {
-  int32_t* tk;  // time << 3 | kind, -1 = no shipment
+  uint8_t* tk;  // (time - t) << 3 | kind, kStagedNone = no shipment
   double* val;
   int64_t stride;
-  HeapView scr;  // the heap staging area, scratch for sc_split_scratch while a node acts
+  HeapView8 scr;  // the heap staging area, scratch for sc_split_scratch while a node acts
+  int32_t t;      // the step's time: shipments are stored relative to it
 
   static constexpr bool kUnroll = true;  // a store per destination
   static constexpr bool kLdsSplit = true;
@@ -55,37 +75,43 @@ struct StagedInbox {
   // noship_all: one store per destination and product in all), instead of a clear of the
   // node's every entry before it acts followed by the shipments' stores over most of them.
   static constexpr bool kClearInAct = SCG_STAGED_NOSHIP != 0;
+  // the split's sorted values go to the amounts' slots (a float is exact in the double),
+  // each read back before the amount of its rank overwrites it
   __host__ __device__ __forceinline__ void scratch_put_value(int s, float v) const {
-    scr.tk[s * scr.stride] = sc_f2i(v);
+    scr.val[s * scr.stride] = static_cast<double>(v);
   }
-  __host__ __device__ __forceinline__ float scratch_value(int s) const { return sc_i2f(scr.tk[s * scr.stride]); }
+  __host__ __device__ __forceinline__ float scratch_value(int s) const {
+    return static_cast<float>(scr.val[s * scr.stride]);
+  }
   __host__ __device__ __forceinline__ void scratch_put(int s, Num x) const {
-    scr.tk[s * scr.stride] = x.k;
+    scr.tk[s * scr.stride] = static_cast<uint8_t>(x.k);
     scr.val[s * scr.stride] = x.v;
   }
   __host__ __device__ __forceinline__ Num scratch_get(int s) const {
-    return Num{scr.val[s * scr.stride], scr.tk[s * scr.stride]};
+    return Num{scr.val[s * scr.stride], static_cast<int>(scr.tk[s * scr.stride])};
   }
   __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv&, int src, int d, int /*dest*/, int p,
                                                 int32_t time, Num amount) const {
     ScNode& nd = c.nodes[src];
     const int64_t q = nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d];
-    tk[q * stride] = he_pack(time, amount.k);
+    tk[q * stride] = static_cast<uint8_t>(he_pack(time - t, amount.k));
     val[q * stride] = amount.v;
   }
   __host__ __device__ __forceinline__ void noship(const ScCtx& c, int src, int d, int p) const {
     ScNode& nd = c.nodes[src];
-    tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = -1;
+    tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = kStagedNone;
   }
   __host__ __device__ __forceinline__ void noship_all(const ScCtx& c, int src, int p) const {
     ScNode& nd = c.nodes[src];
-    for (int d = 0; d < nd.n_dests; ++d) tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = -1;
+    for (int d = 0; d < nd.n_dests; ++d)
+      tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = kStagedNone;
   }
   // node src ships nothing this step unless its act writes an entry
   __host__ __device__ __forceinline__ void clear(const ScCtx& c, int src) const {
     ScNode& nd = c.nodes[src];
     for (int d = 0; d < nd.n_dests; ++d)
-      for (int p = 0; p < c.P; ++p) tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = -1;
+      for (int p = 0; p < c.P; ++p)
+        tk[(nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d]) * stride] = kStagedNone;
   }
 };
 
@@ -96,7 +122,7 @@ struct StagedInbox {
 // then, the heap being final for the step, its in-transit bins (:445-461). Heap storage
 // order is the reference's: the same pushes and pops happen in the same order.
 template <class Sink>
-__host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
+__host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const HeapView8& lh, const StagedInbox& in,
                                                WordCache& ltc, const float* act, int t, int i, int p, int& a_i,
                                                int& lt_i, Sink& out, ScAcc& scg_acc_) {
   ScNode& nd = c.nodes[i];
@@ -117,6 +143,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 #define SCG_STAGED_PLAIN 1
 #endif
   const int64_t q0 = nd.in_base + static_cast<int64_t>(p) * nd.in_deg;
+  const int32_t t0 = t << 3;  // an absolute time<<3|kind minus t0 is the relative one
   HeapEntry ib[kChunk];
 #pragma unroll
   for (int u = 0; u < kChunk; ++u)
@@ -133,7 +160,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 #pragma unroll
   for (int u = 0; u < kHeapChunk; ++u)
     if (u < sz) {
-      lh.put(u, b[u]);
+      lh.put(u, HeapEntry{b[u].tk - t0, b[u].v});
       plain &= he_plain(b[u].tk);
     }
   for (int j0 = kHeapChunk; j0 < sz; j0 += kHeapChunk) {
@@ -143,7 +170,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 #pragma unroll
     for (int u = 0; u < kHeapChunk; ++u)
       if (j0 + u < sz) {
-        lh.put(j0 + u, b[u]);
+        lh.put(j0 + u, HeapEntry{b[u].tk - t0, b[u].v});
         plain &= he_plain(b[u].tk);
       }
   }
@@ -157,7 +184,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
     }
 #pragma unroll
     for (int u = 0; u < kChunk; ++u)  // in source order (:347)
-      if (k0 + u < nd.in_deg && ib[u].tk >= 0) {
+      if (k0 + u < nd.in_deg && ib[u].tk != kStagedNone) {
         plain &= he_plain(ib[u].tk);
         if (!py_heappush(lh, sz, c.H, ib[u])) g.overflow = 1;
       }
@@ -167,24 +194,25 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
   // a Python int or float amount (a wave-uniform choice, so no lane runs both bodies)
 #if SCG_STAGED_PLAIN && defined(__HIP_DEVICE_COMPILE__)
   if (__all(plain))
-    st = st0 + sc_receive<true>(lh, sz, t);
+    st = st0 + sc_receive<true>(lh, sz, 0);
   else
-    st = st0 + sc_receive(lh, sz, t);
+    st = st0 + sc_receive(lh, sz, 0);
 #else
-  st = st0 + (SCG_STAGED_PLAIN && plain ? sc_receive<true>(lh, sz, t) : sc_receive(lh, sz, t));
+  st = st0 + (SCG_STAGED_PLAIN && plain ? sc_receive<true>(lh, sz, 0) : sc_receive(lh, sz, 0));
 #endif
   SCG_ACC(2);
   if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) {
     const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));
     ++a_i;
     if (np_lt(pyint(0), amount)) {
-      const HeapEntry e{he_pack(t + node_leadtime(c, g, ltc, nd, t, lt_i), amount.k), amount.v};
+      const HeapEntry e{he_pack(node_leadtime(c, g, ltc, nd, t, lt_i), amount.k), amount.v};  // relative
       if (!py_heappush(lh, sz, c.H, e)) g.overflow = 1;
       ++lt_i;
     }
   }
   SCG_ACC(3);
-  sc_observe_bins(c, lh, sz, t, i, p, out, [&](int k, const HeapEntry& e) { gh.put(k, e); });  // copy back
+  // relative times: the step is time 0; the copy back makes them absolute again
+  sc_observe_bins(c, lh, sz, 0, i, p, out, [&](int k, const HeapEntry& e) { gh.put(k, HeapEntry{e.tk + t0, e.v}); });
   gsz = sz;
   SCG_ACC(4);
 }
@@ -197,7 +225,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 // time-to-go ones). Returns the reward. (Staging the node's stocks in LDS as well measured
 // no faster on MI355X: stock accesses are few and cache-resident.)
 template <int MAXD, class Sink>
-__host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView& lh, const StagedInbox& in,
+__host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView8& lh, const StagedInbox& in,
                                                  const float* act, int t, Sink& out) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   Num total = pyint(0);

@@ -327,7 +327,7 @@ class SupplyChainVecEnv:
         self._err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._inbox_tk = self._inbox_val = None
         if self.kernel == "staged":  # shipments in flight within a step [inbox_size][N]
-            self._inbox_tk = torch.zeros((max(c.inbox_size, 1), n_envs), dtype=torch.int32, device=dev)
+            self._inbox_tk = torch.zeros((max(c.inbox_size, 1), n_envs), dtype=torch.uint8, device=dev)
             self._inbox_val = torch.zeros((max(c.inbox_size, 1), n_envs), dtype=torch.float64, device=dev)
         self._ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None
         self._final_ret = torch.zeros(n_envs, dtype=torch.float64, device=dev) if track_returns else None

@@ -392,7 +392,7 @@ typedef struct scg_sc_state {
   double* episode_return;       /* [N] optional                                             */
   double* final_return;         /* [N] optional: return at the terminal step                */
   int32_t* error_flags;         /* [1] DEVICE, sticky: bit 0 = a heap exceeded capacity    */
-  int32_t* inbox_tk;            /* [inbox_size][N] staged kernel: shipment time<<3|kind, -1 = none */
+  uint8_t* inbox_tk;            /* [inbox_size][N] staged kernel: shipment (time - t)<<3|kind, 0xFF = none */
   double* inbox_val;            /* [inbox_size][N] staged kernel: shipment amount               */
   /* build_info ledgers, info['sc_episode'] (:684-695, :750-760): optional (every kernel but
      the level kernel).

@@ -93,10 +93,11 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
     const float* a = actions + static_cast<int64_t>(t - 1) * c.A;
     if (mode == 2) {  // sc_step_staged_kernel: one node's heaps staged, shipments via the inbox
       const int slots = std::max(c.H, scg::sc_maxd_bucket(cfg->max_dests));  // heap or split scratch
-      std::vector<int32_t> ltk(slots, 0x7fffffff), inbox_tk(cfg->inbox_size > 0 ? cfg->inbox_size : 1, 0x7fffffff);
+      // byte-packed entries (0xEE: garbage until written)
+      std::vector<uint8_t> ltk(slots, 0xEE), inbox_tk(cfg->inbox_size > 0 ? cfg->inbox_size : 1, 0xEE);
       std::vector<double> lval(slots, -1.0), inbox_val(inbox_tk.size(), -1.0);
-      const scg::HeapView loc{ltk.data(), lval.data(), 1};
-      const scg::StagedInbox in{inbox_tk.data(), inbox_val.data(), 1, loc};
+      const scg::HeapView8 loc{ltk.data(), lval.data(), 1};
+      const scg::StagedInbox in{inbox_tk.data(), inbox_val.data(), 1, loc, t};
       double* row = obs + static_cast<int64_t>(t) * c.O;
       auto out = [row](int o, double v) { row[o] = v; };
       double r = 0.0;
