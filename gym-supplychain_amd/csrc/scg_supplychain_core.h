@@ -119,9 +119,11 @@ enum ScLedgerKey : int {
 // the episode ledger as _update_statistics does (:750-760): the reference sums the nodes'
 // entries after the step in node order, and each entry is set at most once per act, so
 // adding it where it is set gives the same sums; entries an act leaves at the Python int 0
-// change neither value nor type of a sum, so they are skipped.
+// change neither value nor type of a sum, so they are skipped — and so is an entry the act
+// sets to the Python int 0 (a penalty of nothing: int 0 + x is x, value and type).
 __host__ __device__ __forceinline__ void sc_note(const ScCtx& c, ScEnv& e, int key, int p, Num cost, Num units) {
   if (!e.led_v) return;
+  if (cost.k == NK_INT && units.k == NK_INT && cost.v == 0.0 && units.v == 0.0) return;
   if (e.led_word) {  // by node: the slot of this node's entry, reduced in node order later
     const int64_t s0 = ((static_cast<int64_t>(e.led_node) * 2 * SCG_SC_LEDGER_KEYS + key) * c.P + p) * e.led_stride + e.soff;
     const int64_t s1 = s0 + static_cast<int64_t>(SCG_SC_LEDGER_KEYS) * c.P * e.led_stride;

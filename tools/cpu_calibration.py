@@ -1,13 +1,14 @@
 """Calibrate bench.py's cpu_baseline worker against the reference — build container only.
 
-    python tools/cpu_calibration.py [--seconds 2.0] [--reps 5]
+    python tools/cpu_calibration.py [--seconds 6.0] [--reps 7] [--cpu K]
 
 BASELINE.md:62 asks that the restatement timed on the GPU box (oracle.beergame.
 BeerGameOracle, the "reference NumPy step()") run within +-15 % of the reference's own
 BeerGameEnv per core. This times both with bench.py's worker loop on one core — per episode:
 construct the env with that episode's customer_demand, reset(), 35 step() calls on
-pre-drawn actions — alternating them `--reps` times, and prints one JSON line with both
-rates and their ratio. The reference is imported read-only from /root/reference with the
+pre-drawn actions — alternating them `--reps` times (pinned to one core), and prints one JSON
+line with both median rates, their ratio and the median of the per-pair ratios (each pair
+ran back to back, so host drift cancels in it). The reference is imported read-only from /root/reference with the
 gym stand-in of oracle/refharness/; without it the script exits.
 """
 import argparse
@@ -39,9 +40,12 @@ def rate(make_env, demands, acts, seconds):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--seconds", type=float, default=2.0)
-    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--seconds", type=float, default=6.0)
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--cpu", type=int, default=None, help="core to pin to (default: the last one available)")
     a = ap.parse_args()
+    cpus = sorted(os.sched_getaffinity(0))
+    os.sched_setaffinity(0, {cpus[-1] if a.cpu is None else a.cpu})
     if not os.path.isdir(REFERENCE):
         print(f"{REFERENCE} absent")
         return
@@ -57,8 +61,11 @@ def main():
     for _ in range(a.reps):
         ref.append(rate(BeerGameEnv, demands, acts, a.seconds))
         port.append(rate(BeerGameOracle, demands, acts, a.seconds))
+    pairs = [p / r for p, r in zip(port, ref)]
     out = dict(reference_steps_per_s=statistics.median(ref), port_steps_per_s=statistics.median(port),
                ratio_port_over_reference=statistics.median(port) / statistics.median(ref),
+               median_pair_ratio=statistics.median(pairs), pair_ratios=pairs,
+               within_15pct=all(0.85 <= x <= 1.15 for x in (statistics.median(pairs),)),
                reference_runs=ref, port_runs=port, cores=1, seconds_per_run=a.seconds,
                numpy=np.__version__, python=sys.version.split()[0])
     print(json.dumps(out))
