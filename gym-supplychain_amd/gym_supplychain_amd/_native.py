@@ -16,7 +16,7 @@ import torch  # noqa: F401  (loads the HIP runtime libscgpu.so binds to)
 
 LIB_NAME = "libscgpu.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 SCG_OK = 0
 SCG_ERR_INVALID = 1

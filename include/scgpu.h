@@ -35,7 +35,9 @@
 extern "C" {
 #endif
 
-#define SCG_ABI_VERSION 4
+/* 5 (round 4): scg_sc_state.inbox_tk is uint8 [inbox_size][N] (byte-packed entries);
+ *   shipment delays up to SCG_BG_MAX_DELAY = 4096; full_table of any row count. */
+#define SCG_ABI_VERSION 5
 
 #if defined(__GNUC__)
 #define SCG_API __attribute__((visibility("default")))
