@@ -201,7 +201,7 @@ def cpu_baseline(budget_s=1.5, max_procs=16):
             "sample": f"{procs} processes x {budget_s:.1f} s of beergame-v0 episodes (construct + reset + 35 steps; "
                       f"Poisson(8) demand, uniform [0,8] actions drawn before timing), one env per process, "
                       f"oracle.beergame.BeerGameOracle (the reference step() statement for statement; "
-                      f"profiles/r02_cpu_calibration.json); {steps} env-steps total"}
+                      f"profiles/r04_cpu_calibration.json); {steps} env-steps total"}
 
 
 # ---- the step loop (GPU VecEnv, or a CPU stand-in in tests/test_bench_distributed.py) -----

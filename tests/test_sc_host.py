@@ -230,3 +230,32 @@ def test_auto_kernel_choice():
     assert c.kernel == nat.SC_KERNEL_LANE and c.inbox_size == 0
     _, c, _, _ = _setup(load_sc("ntom"), nat.SC_KERNEL_AUTO)
     assert c.kernel == nat.SC_KERNEL_STAGED and c.inbox_size > 0
+
+
+@pytest.mark.parametrize("lt", [30, 31])
+def test_staged_kernel_takes_lead_times_its_bytes_hold(lt):
+    """The staged kernel's byte-packed entries hold times up to 30 steps after the step's own
+    (scg_supplychain_staged.h): scg_sc_prepare refuses kernel='staged' past that, and
+    kernel='auto' never picks it there."""
+    import ctypes
+    from gym_supplychain_amd import _native as nat
+    from gym_supplychain_amd.envs import SupplyChainSpec
+    meta = load_sc("2perstage")["meta"]
+    kw = dict(meta["kwargs"], stochastic_leadtimes=False, avg_leadtime=lt, max_leadtime=lt)
+    spec = SupplyChainSpec(meta["nodes_info"], **kw)
+    for kernel in (nat.SC_KERNEL_STAGED, nat.SC_KERNEL_AUTO):
+        c = nat.ScConfig()
+        c.n_nodes, c.n_products, c.n_retailers = len(spec.nodes), spec.P, spec.n_retailers
+        c.total_time_steps, c.avg_leadtime, c.max_leadtime = spec.total_time_steps, lt, lt
+        c.demand_lo, c.demand_hi = spec.demand_models[0].lo, spec.demand_models[0].hi
+        for k, v in spec.penalties.items():
+            setattr(c, k, v)
+        c.kernel = kernel
+        rc = nat.lib.scg_sc_prepare(ctypes.byref(c), spec.node_table())
+        if kernel == nat.SC_KERNEL_STAGED:
+            if lt <= 30:
+                assert rc == 0 and c.kernel == nat.SC_KERNEL_STAGED, nat.last_error()
+            else:
+                assert rc == nat.SCG_ERR_INVALID and "lead times" in nat.last_error()
+        else:
+            assert rc == 0 and (lt <= 30 or c.kernel != nat.SC_KERNEL_STAGED)
