@@ -151,45 +151,23 @@ __host__ __device__ __forceinline__ void sc_led_begin_node(const ScCtx& c, ScEnv
   for (int p = 0; p < c.P; ++p) e.led_word[(static_cast<int64_t>(node) * c.P + p) * e.led_word_stride] = 0;
 }
 
-// Whether node nd's act can note a ledger entry `key` for product p other than the Python
-// int 0 (which sc_note skips): a superset of what SC_Node.act sets (:236-394), from the node's
-// role alone — penalties of stock for every node, of processing only where there is
-// processing (a non-factory's over_proc stays the int 0), shipping for every shipping node.
-__host__ __device__ __forceinline__ bool sc_node_notes(ScNode& nd, int key, int p) {
-  switch (key) {
-    case LK_STOCK:
-    case LK_STOCK_PEN: return true;
-    case LK_SUPPLY: return nd.n_supply > 0 && nd.supply_capacity[p] > 0;
-    case LK_PROCESS:
-    case LK_PROCESS_PEN: return !nd.last_level && nd.processing_capacity > 0;
-    case LK_SHIP:
-    case LK_SHIP_PEN: return !nd.last_level;
-    default: return nd.last_level != 0;  // LK_UNMET
-  }
-}
-
 // Ledger entry q = (part * 8 + key) * P + p of one env after the step: the nodes' marked
 // entries added in node order (:750-760) to (lv, lk). cv: the slot values (stride cstride);
 // words: the per-(node, product) marks and types (stride wstride). The slots of a batch of
-// nodes are requested together, so the chain of adds waits on memory once per batch; a node
-// whose role never sets this entry is skipped (a wave-uniform test: no load, no add).
+// nodes are requested together, so the chain of adds waits on memory once per batch.
 __host__ __device__ inline void sc_ledger_reduce(const ScCtx& c, int q, const double* cv, int64_t cstride,
                                                  const uint64_t* words, int64_t wstride, double& lv, int32_t& lk) {
   const int p = q % c.P, pk = q / c.P;  // pk = part * 8 + key
-  const int key = pk % SCG_SC_LEDGER_KEYS;
   constexpr int kBatch = 8;
   Num acc{lv, np_kind_int(lk)};
   for (int i0 = 0; i0 < c.n_nodes; i0 += kBatch) {
     double v[kBatch];
-    bool may[kBatch];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u)
+      if (i0 + u < c.n_nodes) v[u] = cv[((static_cast<int64_t>(i0 + u) * 2 * SCG_SC_LEDGER_KEYS + pk) * c.P + p) * cstride];
 #pragma unroll
     for (int u = 0; u < kBatch; ++u) {
-      may[u] = i0 + u < c.n_nodes && sc_node_notes(c.nodes[i0 + u], key, p);
-      if (may[u]) v[u] = cv[((static_cast<int64_t>(i0 + u) * 2 * SCG_SC_LEDGER_KEYS + pk) * c.P + p) * cstride];
-    }
-#pragma unroll
-    for (int u = 0; u < kBatch; ++u) {
-      if (!may[u]) continue;
+      if (i0 + u >= c.n_nodes) break;
       const uint64_t w = words[(static_cast<int64_t>(i0 + u) * c.P + p) * wstride];
       if ((w >> pk) & 1) acc = np_add(acc, Num{v[u], np_kind_int(static_cast<int>((w >> (16 + 3 * pk)) & 7))});
     }
