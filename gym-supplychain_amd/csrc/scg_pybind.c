@@ -41,6 +41,35 @@ static PyObject* bg_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs
   return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
 }
 
+/* A vec env's fixed step arguments, filled once by the Python side (its address is the
+ * handle): bg_step_h(handle, action, stream) then parses three arguments per step. */
+typedef struct bg_step_args {
+  uint64_t cfg, state, obs, reward, terminal_obs;
+  uint32_t flags;
+} bg_step_args;
+
+/* bg_step_h(handle, action, stream) */
+static PyObject* bg_step_h(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  void* p[3];
+  if (nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "bg_step_h expects 3 arguments");
+    return NULL;
+  }
+  for (int i = 0; i < 3; ++i)
+    if (as_ptr(args[i], &p[i])) return NULL;
+  const bg_step_args* h = (const bg_step_args*)p[0];
+  if (!h) {
+    PyErr_SetString(PyExc_ValueError, "bg_step_h: null handle");
+    return NULL;
+  }
+  int32_t done = 0;
+  const int rc = scg_bg_step((const scg_bg_config*)(uintptr_t)h->cfg, (scg_bg_state*)(uintptr_t)h->state,
+                             (const int32_t*)p[1], (int32_t*)(uintptr_t)h->obs, (int32_t*)(uintptr_t)h->reward,
+                             (int32_t*)(uintptr_t)h->terminal_obs, h->flags, &done, p[2]);
+  return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
+}
+
 /* bg_step_timed(cfg, state, action, obs, reward, terminal_obs, flags, start_event, stop_event, stream) */
 static PyObject* bg_step_timed(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
   (void)self;
@@ -76,6 +105,7 @@ static PyObject* sc_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs
 
 static PyMethodDef methods[] = {
     {"bg_step", (PyCFunction)(void (*)(void))bg_step, METH_FASTCALL, "scg_bg_step"},
+    {"bg_step_h", (PyCFunction)(void (*)(void))bg_step_h, METH_FASTCALL, "scg_bg_step with the fixed arguments behind a handle"},
     {"bg_step_timed", (PyCFunction)(void (*)(void))bg_step_timed, METH_FASTCALL, "scg_bg_step_timed"},
     {"sc_step", (PyCFunction)(void (*)(void))sc_step, METH_FASTCALL, "scg_sc_step"},
     {NULL, NULL, 0, NULL},

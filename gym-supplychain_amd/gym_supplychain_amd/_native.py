@@ -273,6 +273,13 @@ except AttributeError:  # pragma: no cover - older torch
     _raw_stream = None
 
 
+class BgStepArgs(ctypes.Structure):
+    """The fixed arguments of a BeerGame step (scg_pybind.c bg_step_args): addresses of the
+    config and state structs and of the output buffers, and the step flags."""
+    _fields_ = [("cfg", ctypes.c_uint64), ("state", ctypes.c_uint64), ("obs", ctypes.c_uint64),
+                ("reward", ctypes.c_uint64), ("terminal_obs", ctypes.c_uint64), ("flags", ctypes.c_uint32)]
+
+
 def raw_stream(device_index):
     if _raw_stream is not None:
         return _raw_stream(device_index)

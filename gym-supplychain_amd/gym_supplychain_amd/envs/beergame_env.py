@@ -274,8 +274,15 @@ class BeerGameVecEnv:
         self._term_ptr = self._term_obs.data_ptr()
         self._cfg_addr, self._st_addr = ctypes.addressof(self._cfg), ctypes.addressof(self._st)
         self._fast_step, self._fast_step_timed = nat.fast.bg_step, nat.fast.bg_step_timed
+        # the fixed arguments of a step behind one handle (scg_pybind.c bg_step_args): the
+        # step loop passes three (flags are fixed per env; the rest are this env's buffers)
+        self._step_args = nat.BgStepArgs(self._cfg_addr, self._st_addr, self._obs_ptr, self._rew_ptr, self._term_ptr,
+                                         self._flags)
+        self._step_handle = ctypes.addressof(self._step_args)
+        self._fast_step_h = nat.fast.bg_step_h
         self._raw_stream = nat.raw_stream_fn()  # torch's current raw stream, one C call
-        self._ready = {}  # id(actions) -> (weakref, data_ptr, stride, shape) of validated action tensors
+        self._ready = {}  # id(actions) -> (weakref, data_ptr) of validated action tensors
+        self._act_numel = n_envs * L
         # gym surface (an extension: the reference leaves both spaces unset, :62-64)
         self.single_observation_space = spaces.Box(_I32[0], _I32[1], (L,), np.int32)
         # actions: the reference's are unbounded int64 (:121); sampled ones stay within
@@ -322,25 +329,24 @@ class BeerGameVecEnv:
 
     def step(self, actions, _events=None):
         # a tensor validated once is recognised by identity and data pointer (the policy's
-        # per-week action buffers are reused), skipping the per-call checks
-        # (shape and stride catch in-place metadata changes that keep the pointer: t_(),
-        # as_strided_(), resize_() to fewer rows)
+        # per-week action buffers are reused), skipping the per-call checks; still contiguous
+        # with N * L elements catches the in-place metadata changes that keep the pointer
+        # (t_(), as_strided_(), resize_() to fewer rows) — any contiguous int32 buffer of
+        # N * L elements is read as [N, L], as _actions() reshapes it
         ok = self._ready.get(id(actions))
-        if ok is not None and ok[0]() is actions and ok[1] == actions.data_ptr() and ok[2] == actions.stride() \
-                and ok[3] == actions.shape:
+        if ok is not None and ok[0]() is actions and ok[1] == actions.data_ptr() and actions.is_contiguous() \
+                and actions.numel() == self._act_numel:
             ptr = ok[1]
         else:
             if self._is_ready(actions):
                 if len(self._ready) >= 64:
                     self._ready.clear()
-                self._ready[id(actions)] = (weakref.ref(actions), actions.data_ptr(), actions.stride(),
-                                         actions.shape)
+                self._ready[id(actions)] = (weakref.ref(actions), actions.data_ptr())
             else:
                 actions = self._actions(actions)
             ptr = actions.data_ptr()
         if _events is None:
-            r = self._fast_step(self._cfg_addr, self._st_addr, ptr, self._obs_ptr, self._rew_ptr,
-                                self._term_ptr, self._flags, self._raw_stream(self._dev_index))
+            r = self._fast_step_h(self._step_handle, ptr, self._raw_stream(self._dev_index))
         else:  # (start, stop) hipEvent_t handles stamped with the kernel's own dispatch times
             r = self._fast_step_timed(self._cfg_addr, self._st_addr, ptr, self._obs_ptr,
                                       self._rew_ptr, self._term_ptr, self._flags, _events[0], _events[1],
