@@ -245,14 +245,14 @@ def region(loop, k, world, barrier, sync, stamps=None, split=None):
     `split`, also its host side: split["enqueue_s"] = the step loop's wall time up to the
     final synchronize (the host enqueueing k launches), split["drain_s"] = the rest (the
     synchronize waiting for the GPU, and the closing barrier)."""
-    if world > 1:
+    if barrier is not None:
         barrier()
     sync()
     t0 = time.perf_counter()
     loop.run(k, first=stamps[0] if stamps else None, last=stamps[1] if stamps else None)
     t1 = time.perf_counter()
     sync()
-    if world > 1:
+    if barrier is not None:
         barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = stamps[2](stamps[0], stamps[1]) if stamps else None
@@ -261,9 +261,10 @@ def region(loop, k, world, barrier, sync, stamps=None, split=None):
     return elapsed, gpu_ms
 
 
-def max_over_ranks(values, world, device):
-    """Elementwise max of a list of floats over ranks (all_reduce MAX; None stays None)."""
-    if world == 1:
+def max_over_ranks(values, world, device, collective=None):
+    """Elementwise max of a list of floats over ranks (all_reduce MAX; None stays None).
+    collective: run the all_reduce even on one rank (the rehearsal, GpuPlatform)."""
+    if not (world > 1 if collective is None else collective):
         return values
     import torch
     import torch.distributed as dist
@@ -363,6 +364,7 @@ class Platform:
     events. GpuPlatform is the real one; tests/test_bench_distributed.py runs the same flow
     (run()) on gloo ranks with a CPU stand-in."""
     world, rank, device = 1, 0, None
+    collectives = False  # barriers, max over ranks and the return all-gather run (world > 1)
 
     def make_env(self, n_envs, env_offset):
         raise NotImplementedError
@@ -400,7 +402,10 @@ class GpuPlatform(Platform):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world > 1:
+        # SCG_BENCH_PG=1 (under torch.distributed.run, one rank): the process group and every
+        # RCCL call of the flow run at N = 1 too, a rehearsal of the multi-GPU path on one GPU
+        self.collectives = self.world > 1 or os.environ.get("SCG_BENCH_PG") == "1"
+        if self.collectives:
             torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         self.device = torch.device("cuda", local_rank)
@@ -448,7 +453,8 @@ def run(args, plat):
     world, rank, device = plat.world, plat.rank, plat.device
     N = args.envs
     env = plat.make_env(N, shard_offset(N, rank))
-    gather = EpisodeReturnGather(N, device)
+    coll = world > 1 or plat.collectives
+    gather = EpisodeReturnGather(N, device, collective=coll)
     env.reset()
     loop = StepLoop(env, plat.week_actions(env, N), gather)
     plan = list(env._plan)
@@ -460,7 +466,7 @@ def run(args, plat):
         w0 = env.week
         return sum(week_bytes((w0 + i) % WEEKS + 1) for i in range(k))
 
-    barrier = plat.barrier if world > 1 else None
+    barrier = plat.barrier if coll else None
     ev = [plat.new_event() for _ in range(4)]
 
     warmup_run = max(args.warmup, WEEKS)
@@ -495,7 +501,7 @@ def run(args, plat):
         plat.destroy_event(e)
     env.check_errors()
     elapsed, ep_elapsed, ep_gpu_ms, iso_ms, enq_s, drain_s, empty = max_over_ranks(
-        [elapsed, ep_elapsed, ep_gpu_ms, iso_ms, split["enqueue_s"], split["drain_s"], empty], world, device)
+        [elapsed, ep_elapsed, ep_gpu_ms, iso_ms, split["enqueue_s"], split["drain_s"], empty], world, device, coll)
     extras = plat.extras() if rank == 0 and world == 1 and not args.no_extras else {}
     if rank != 0:
         return None
@@ -532,7 +538,7 @@ def run(args, plat):
         "data": "synthetic: Poisson(8) demand drawn on device (Philox4x32-10), uniform int [0,8] actions",
         "config": {"workload": "beergame-v0 step() x 65536 envs/GPU (BASELINE configs[1]; configs[4] at N=8)",
                    "n_envs_per_gpu": N, "levels": LEVELS, "weeks": WEEKS, "auto_reset": True,
-                   "ledgers": True, "orders_history": True, "episode_return_allgather": world > 1,
+                   "ledgers": True, "orders_history": True, "episode_return_allgather": coll,
                    "parallelism": f"env-shard x{world}"},
         "episodes_timed": {"episodes": EPISODES_TIMED, "steps": k_ep, "value": N * world * k_ep / ep_elapsed,
                            "ms_per_step": ep_elapsed * 1e3 / k_ep, "avg_kernel_us": ep_gpu_ms * 1e3 / k_ep,
@@ -558,7 +564,7 @@ def main(argv=None):
     line = run(args, plat)
     if line is not None:
         print(json.dumps(line), flush=True)
-    if plat.world > 1:
+    if plat.collectives:
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -74,21 +74,25 @@ class EpisodeReturnGather:
     on_episode_end(final_return) snapshots the per-env int64 returns on the producing
     stream (so the next episode may overwrite the env's buffer) and launches an async
     all-gather; result() waits for the latest one and returns the global [world * N]
-    tensor. With one process it degenerates to the snapshot.
+    tensor. With one process it degenerates to the snapshot, unless `collective` asks for
+    the all-gather anyway (a one-rank rehearsal of the RCCL path; default: world > 1).
     """
 
-    def __init__(self, n_per_rank, device, group=None):
+    def __init__(self, n_per_rank, device, group=None, collective=None):
         self.rank, self.world = rank_world()
         self.group = group
         self.n = int(n_per_rank)
         self.device = torch.device(device)
-        self._stage = torch.zeros(self.n, dtype=torch.int64, device=self.device) if self.world > 1 else None
+        self.collective = self.world > 1 if collective is None else bool(collective)
+        if self.collective and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("the return all-gather needs an initialised torch.distributed process group")
+        self._stage = torch.zeros(self.n, dtype=torch.int64, device=self.device) if self.collective else None
         self._out = torch.zeros(self.world * self.n, dtype=torch.int64, device=self.device)
         self._work = None
         self.gathers = 0
 
     def on_episode_end(self, final_return):
-        if self.world == 1:  # the snapshot is the result: one device copy per episode
+        if not self.collective:  # the snapshot is the result: one device copy per episode
             _async_copy(self._out, final_return)
             self.gathers += 1
             return

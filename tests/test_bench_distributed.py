@@ -123,9 +123,10 @@ class CpuPlatform:
     """bench.Platform for CPU ranks: the stand-in batch env, gloo collectives, wall-clock
     events stamped by the stand-in's step."""
 
-    def __init__(self, world, rank):
+    def __init__(self, world, rank, collectives=None):
         import bench
         self.world, self.rank, self.device = world, rank, "cpu"
+        self.collectives = world > 1 if collectives is None else collectives
         self._base = bench.Platform()
 
     def make_env(self, n_envs, env_offset):
@@ -178,7 +179,7 @@ class StampedBatch(CpuBeerGameBatch):
         pass
 
 
-def _run_worker(rank, world, port, q):
+def _run_worker(rank, world, port, q, collectives=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -196,7 +197,7 @@ def _run_worker(rank, world, port, q):
                 super().on_episode_end(final_return)
 
         gd.EpisodeReturnGather = RecordingGather
-        plat = CpuPlatform(world, rank)
+        plat = CpuPlatform(world, rank, collectives)
         args = bench.parse_args(["--gpus", str(world), "--envs", "2", "--steps", "20", "--warmup", "5",
                                  "--kernel-samples", "35", "--no-extras", "--no-cpu-baseline"])
         line = bench.run(args, plat)
@@ -207,16 +208,17 @@ def _run_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_bench_run_emits_the_rank0_line(world):
     """bench.run() on `world` gloo ranks (the 8-rank case is the driver's 8-GPU launch shape):
     global shard offsets, every rank's all-gather holding the shards in rank order, and rank
-    0's line (n_gpus, whole-job value)."""
+    0's line (n_gpus, whole-job value). World 1 is the one-rank rehearsal (SCG_BENCH_PG=1 on
+    a GPU box): a process group, and every barrier and collective of the flow run anyway."""
     import json
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_run_worker, args=(r, world, port, q, True)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in procs)
