@@ -7,10 +7,13 @@
  *
  * Return value: (status << 1) | done; status != 0 is turned into the mapped Python
  * exception by the caller (gym_supplychain_amd._native.check).
+ *
+ * Plus node_barrier, the host barrier of bench.py's ranks on one node (below).
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <stdint.h>
+#include <time.h>
 
 #include "scgpu.h"
 
@@ -103,11 +106,66 @@ static PyObject* sc_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs
   return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
 }
 
+static int64_t now_us(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000 + ts.tv_nsec / 1000;
+}
+
+/* node_barrier(words, world, sense, timeout_us) -> the new sense. A sense-reversing barrier
+ * of `world` processes of one node on two int32 words of a shared page: words[0] counts
+ * arrivals, words[1] is the phase. Every rank passes its last returned sense (0 at first);
+ * the last to arrive resets the count and flips the phase, the others spin until it flips.
+ * TimeoutError after timeout_us (a rank that never comes). The GIL is released while
+ * waiting. */
+static PyObject* node_barrier(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  void* p;
+  if (nargs != 4) {
+    PyErr_SetString(PyExc_TypeError, "node_barrier expects 4 arguments");
+    return NULL;
+  }
+  if (as_ptr(args[0], &p)) return NULL;
+  const long world = PyLong_AsLong(args[1]);
+  const long old = PyLong_AsLong(args[2]);
+  const long long timeout_us = PyLong_AsLongLong(args[3]);
+  if (PyErr_Occurred()) return NULL;
+  if (!p || world < 1) {
+    PyErr_SetString(PyExc_ValueError, "node_barrier: null page or world < 1");
+    return NULL;
+  }
+  int32_t* w = (int32_t*)p;
+  const int32_t sense = old ? 0 : 1;
+  int timed_out = 0;
+  Py_BEGIN_ALLOW_THREADS
+  if (__atomic_fetch_add(&w[0], 1, __ATOMIC_ACQ_REL) == world - 1) {
+    __atomic_store_n(&w[0], 0, __ATOMIC_RELAXED);
+    __atomic_store_n(&w[1], sense, __ATOMIC_RELEASE);
+  } else {
+    const int64_t t0 = now_us();
+    unsigned spins = 0;
+    while (__atomic_load_n(&w[1], __ATOMIC_ACQUIRE) != sense) {
+      if ((++spins & 1023u) == 0 && now_us() - t0 > timeout_us) {
+        timed_out = 1;
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+  }
+  Py_END_ALLOW_THREADS
+  if (timed_out) {
+    PyErr_SetString(PyExc_TimeoutError, "node_barrier: not every rank arrived");
+    return NULL;
+  }
+  return PyLong_FromLong(sense);
+}
+
 static PyMethodDef methods[] = {
     {"bg_step", (PyCFunction)(void (*)(void))bg_step, METH_FASTCALL, "scg_bg_step"},
     {"bg_step_h", (PyCFunction)(void (*)(void))bg_step_h, METH_FASTCALL, "scg_bg_step with the fixed arguments behind a handle"},
     {"bg_step_timed", (PyCFunction)(void (*)(void))bg_step_timed, METH_FASTCALL, "scg_bg_step_timed"},
     {"sc_step", (PyCFunction)(void (*)(void))sc_step, METH_FASTCALL, "scg_sc_step"},
+    {"node_barrier", (PyCFunction)(void (*)(void))node_barrier, METH_FASTCALL, "host barrier of one node's ranks"},
     {NULL, NULL, 0, NULL},
 };
 

@@ -8,6 +8,7 @@ end-of-episode metric gather, an RCCL all-gather over xGMI issued asynchronously
 overlaps the next episode's steps (the north star's "all-gather for the end-of-episode
 reward/metric reduction").
 """
+import ctypes
 import os
 
 import torch
@@ -68,6 +69,94 @@ def _async_copy(dst, src):
         raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
 
 
+class _RcclAllGather:
+    """An RCCL communicator of our own over torch's librccl, for the episode-return
+    all-gather: ncclAllGather goes straight onto a side HIP stream ordered by two events, with
+    none of torch.distributed's per-collective bookkeeping (Work objects, stream syncs,
+    watchdog records: ≈30 µs of host time per call through dist.all_gather_into_tensor,
+    profiles/r04p_gather_probe.log, against ≈ a launch here). The unique id travels over the
+    torch.distributed group; every rank of the group builds it (a collective)."""
+
+    class _UniqueId(ctypes.Structure):
+        _fields_ = [("internal", ctypes.c_char * 128)]
+
+    NCCL_INT64 = 4
+
+    def __init__(self, group, device):
+        from . import _native as nat
+        lib_dir = os.path.join(os.path.dirname(torch.__file__), "lib")
+        path = os.path.join(lib_dir, "librccl.so")
+        self.lib = lib = ctypes.CDLL(path if os.path.exists(path) else "librccl.so")
+        lib.ncclGetUniqueId.argtypes = [ctypes.POINTER(self._UniqueId)]
+        lib.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, self._UniqueId, ctypes.c_int]
+        lib.ncclAllGather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_void_p]
+        lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        lib.ncclGetErrorString.restype = ctypes.c_char_p
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = self._UniqueId()
+        if rank == 0:
+            self._check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        box = [bytes(uid) if rank == 0 else None]  # the raw 128 bytes (the field reads up to a NUL)
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(box, src=src, group=group, device=device)
+        uid = self._UniqueId.from_buffer_copy(box[0])
+        self.comm = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            self._check(lib.ncclCommInitRank(ctypes.byref(self.comm), world, uid, rank), "ncclCommInitRank")
+            self.stream = torch.cuda.Stream(device)  # from torch's pool: non-blocking
+        hip = nat.hip_runtime()
+        hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        hip.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        self.hip = hip
+        self._src = (None, None)  # (tensor, data_ptr) of the last snapshot source, checked once
+        self.ready, self.done = ctypes.c_void_p(), ctypes.c_void_p()
+        for ev in (self.ready, self.done):  # hipEventDisableTiming: a record is a marker only
+            if hip.hipEventCreateWithFlags(ctypes.byref(ev), 2) != 0:
+                raise RuntimeError("hipEventCreateWithFlags failed")
+        self.gstream = ctypes.c_void_p(self.stream.cuda_stream)
+        self.pending = False
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.lib.ncclGetErrorString(rc).decode()} ({rc})")
+
+    def gather(self, out, stage, src, stream):
+        """out <- all ranks' src (via stage), ordered after the work on `stream` (raw handle)
+        and, for the next snapshot into stage, before it."""
+        hip = self.hip
+        if self._src[0] is not src or self._src[1] != src.data_ptr():
+            if not (src.is_cuda and src.is_contiguous() and src.dtype == stage.dtype and src.numel() == stage.numel()
+                    and src.device == stage.device):
+                raise ValueError("the returns to gather must be a contiguous int64 tensor of n_per_rank on the device")
+            self._src = (src, src.data_ptr())
+        if self.pending:  # the previous gather may still read stage
+            hip.hipStreamWaitEvent(stream, self.done, 0)
+        if hip.hipMemcpyAsync(stage.data_ptr(), self._src[1], stage.numel() * 8, 3, stream) != 0:  # D2D snapshot
+            raise RuntimeError("hipMemcpyAsync failed")
+        hip.hipEventRecord(self.ready, stream)
+        hip.hipStreamWaitEvent(self.gstream, self.ready, 0)
+        self._check(self.lib.ncclAllGather(stage.data_ptr(), out.data_ptr(), stage.numel(), self.NCCL_INT64,
+                                           self.comm, self.gstream), "ncclAllGather")
+        hip.hipEventRecord(self.done, self.gstream)
+        self.pending = True
+
+    def wait(self, stream):
+        """Order `stream` after the latest gather."""
+        if self.pending:
+            self.hip.hipStreamWaitEvent(stream, self.done, 0)
+            self.pending = False
+
+    def close(self):
+        if self.comm:
+            torch.cuda.current_stream().synchronize()
+            self.stream.synchronize()
+            self.lib.ncclCommDestroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+
 class EpisodeReturnGather:
     """All-gather of every env's finished-episode return, overlapped with compute.
 
@@ -76,6 +165,10 @@ class EpisodeReturnGather:
     all-gather; result() waits for the latest one and returns the global [world * N]
     tensor. With one process it degenerates to the snapshot, unless `collective` asks for
     the all-gather anyway (a one-rank rehearsal of the RCCL path; default: world > 1).
+
+    On GPUs with an nccl (RCCL) group the gather runs on a communicator of its own
+    (_RcclAllGather); SCG_GATHER=torch keeps it on dist.all_gather_into_tensor, which is also
+    the path of any other backend (gloo: the CPU tests).
     """
 
     def __init__(self, n_per_rank, device, group=None, collective=None):
@@ -89,11 +182,20 @@ class EpisodeReturnGather:
         self._stage = torch.zeros(self.n, dtype=torch.int64, device=self.device) if self.collective else None
         self._out = torch.zeros(self.world * self.n, dtype=torch.int64, device=self.device)
         self._work = None
+        self._rccl = None
+        if self.collective and self.device.type == "cuda" and dist.get_backend(group) == "nccl" \
+                and os.environ.get("SCG_GATHER", "rccl") != "torch":
+            self._rccl = _RcclAllGather(group, self.device)
         self.gathers = 0
 
     def on_episode_end(self, final_return):
         if not self.collective:  # the snapshot is the result: one device copy per episode
             _async_copy(self._out, final_return)
+            self.gathers += 1
+            return
+        if self._rccl is not None:
+            from . import _native as nat
+            self._rccl.gather(self._out, self._stage, final_return, nat.raw_stream(self.device.index))
             self.gathers += 1
             return
         if self._work is not None:
@@ -103,7 +205,17 @@ class EpisodeReturnGather:
         self.gathers += 1
 
     def result(self):
+        if self._rccl is not None:
+            from . import _native as nat
+            self._rccl.wait(nat.raw_stream(self.device.index))
+            return self._out
         if self._work is not None:
             self._work.wait()
             self._work = None
         return self._out
+
+    def close(self):
+        """Release the RCCL communicator (synchronises)."""
+        if self._rccl is not None:
+            self._rccl.close()
+            self._rccl = None

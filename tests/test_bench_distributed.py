@@ -256,3 +256,42 @@ def test_bench_run_emits_the_rank0_line(world):
     # the walk to the boundary + 3,500 + 35 isolated steps
     total = 35 + 20 + 20 + (35 - (35 + 20 + 20) % 35) % 35 + 3500 + 35
     assert line["episode_returns_gathered"] == total // 35 == res[0]["ends"]
+
+
+def _barrier_worker(rank, world, port, q, arr, iters):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        bar = bench.NodeBarrier(rank, world, dist.barrier, timeout_s=120)
+        bad = 0
+        for i in range(iters):
+            arr[rank] = i
+            bar()
+            seen = list(arr)
+            bad += (min(seen) < i) or (max(seen) > i + 1)  # nobody passed early, nobody two ahead
+        q.put((rank, bad))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_node_barrier_holds_every_rank(world):
+    """bench.NodeBarrier (the region brackets' barrier on a GPU node): after barrier i every
+    rank has reached iteration i, and no rank is two iterations ahead; its /dev/shm page is
+    unlinked once mapped."""
+    import glob
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    arr = ctx.Array("l", world, lock=False)
+    port = _free_port()
+    before = set(glob.glob("/dev/shm/scg_bench_barrier_*"))
+    procs = [ctx.Process(target=_barrier_worker, args=(r, world, port, q, arr, 2000)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(v == 0 for v in res.values())
+    assert set(glob.glob("/dev/shm/scg_bench_barrier_*")) <= before

@@ -96,3 +96,44 @@ def test_entropy_seed_group_needs_a_process_group():
     with pytest.raises(RuntimeError):
         entropy_seed(None, seed_group=True)
     assert entropy_seed(7, seed_group=True) == 7
+
+
+def _rccl_gather_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    try:
+        from gym_supplychain_amd.distributed import EpisodeReturnGather
+        g = EpisodeReturnGather(4096, dev, collective=True)
+        src = torch.zeros(4096, dtype=torch.int64, device=dev)
+        got = []
+        for k in range(5):
+            src.copy_(torch.arange(4096, device=dev) * (k + 1) - 7)  # the env's buffer, rewritten each episode
+            g.on_episode_end(src)
+            if k % 2:
+                got.append(g.result().clone())  # waited on the current stream, then read
+        got.append(g.result().clone())
+        want = [torch.arange(4096, device=dev) * (k + 1) - 7 for k in (1, 3, 4)]
+        q.put((g._rccl is not None, all(bool((a == b).all()) for a, b in zip(got, want)), g.gathers))
+        g.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_return_gather_on_one_rank():
+    """EpisodeReturnGather on an nccl group runs on its own RCCL communicator (side stream,
+    event-ordered): every result() holds the snapshot of the latest episode end even though
+    the source buffer is rewritten right after."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = ctx.Process(target=_rccl_gather_worker, args=(port, q))
+    p.start()
+    used_rccl, ok, n = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert used_rccl and ok and n == 5
