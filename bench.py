@@ -363,10 +363,11 @@ class NodeBarrier:
     (`_scgpu_fast.node_barrier`, a sense-reversing counter; about a microsecond) instead of an
     RCCL all-reduce plus stream synchronisation (20-60 us on one GPU, profiles/r04o_*), which
     the closing barrier would add to every timed region of an N > 1 line. Rank 0 creates the
-    page in /dev/shm and unlinks it once every rank has it mapped (setup barriers:
-    `dist_barrier`), so nothing is left behind even if a rank dies."""
+    page in /dev/shm and unlinks it once every rank has it mapped, so nothing is left behind
+    even if a rank dies. `agree(ok)` (gym_supplychain_amd.distributed.agree) is the setup's
+    collective: a step that fails on any rank raises OSError on every rank."""
 
-    def __init__(self, rank, world, dist_barrier, timeout_s=600.0):
+    def __init__(self, rank, world, agree, timeout_s=600.0):
         import ctypes
         import mmap
 
@@ -376,23 +377,33 @@ class NodeBarrier:
         self._fast = nat.fast.node_barrier
         path = "/dev/shm/scg_bench_barrier_%s_%s" % (os.environ.get("TORCHELASTIC_RUN_ID", "none"),
                                                       os.environ.get("MASTER_PORT", "0"))
+        ok = True
         if rank == 0:
             try:
-                os.unlink(path)
-            except FileNotFoundError:
-                pass
-            fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
-            os.ftruncate(fd, 64)
-            os.close(fd)
-        dist_barrier()
-        fd = os.open(path, os.O_RDWR)
+                try:
+                    os.unlink(path)
+                except FileNotFoundError:
+                    pass
+                fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+                os.ftruncate(fd, 64)
+                os.close(fd)
+            except OSError:
+                ok = False
+        if not agree(ok):
+            raise OSError("the barrier page could not be created")
         try:
-            self._mm = mmap.mmap(fd, 64)
-        finally:
-            os.close(fd)
-        dist_barrier()
+            fd = os.open(path, os.O_RDWR)
+            try:
+                self._mm = mmap.mmap(fd, 64)
+            finally:
+                os.close(fd)
+        except OSError:
+            ok = False
+        ok = agree(ok)
         if rank == 0:
             os.unlink(path)
+        if not ok:
+            raise OSError("the barrier page could not be mapped on every rank")
         self._words = (ctypes.c_int32 * 2).from_buffer(self._mm)
         self._addr = ctypes.addressof(self._words)
 
@@ -454,10 +465,20 @@ class GpuPlatform(Platform):
         torch.cuda.set_device(self.device)
         from gym_supplychain_amd import _native as nat
         self.nat = nat
-        self._node_barrier = NodeBarrier(self.rank, self.world, dist.barrier) if self.collectives else None
+        self._node_barrier = None
+        if self.collectives:
+            from gym_supplychain_amd.distributed import agree
+            try:
+                self._node_barrier = NodeBarrier(self.rank, self.world, lambda ok: agree(ok, device=self.device))
+            except OSError as exc:  # every rank takes the same branch
+                print(f"bench: node barrier unavailable ({exc}); using dist.barrier", file=sys.stderr)
 
     def barrier(self):
-        self._node_barrier()
+        if self._node_barrier is not None:
+            self._node_barrier()
+        else:
+            import torch.distributed as dist
+            dist.barrier()
 
     def make_env(self, n_envs, env_offset):
         from gym_supplychain_amd import BeerGameVecEnv

@@ -69,6 +69,17 @@ def _async_copy(dst, src):
         raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
 
 
+def agree(ok, group=None, device=None):
+    """True on every rank of the group iff `ok` is true on every rank (an all_reduce MIN; on
+    an nccl group the flag travels on `device`). Every rank must call it: the setup steps
+    below use it so that a failure on any rank takes every rank down the same fallback
+    instead of leaving the others waiting in a collective."""
+    on = device if (device is not None and dist.get_backend(group) == "nccl") else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
 class _RcclAllGather:
     """An RCCL communicator of our own over torch's librccl, for the episode-return
     all-gather: ncclAllGather goes straight onto a side HIP stream ordered by two events, with
@@ -84,9 +95,16 @@ class _RcclAllGather:
 
     def __init__(self, group, device):
         from . import _native as nat
+        self.comm = ctypes.c_void_p()
         lib_dir = os.path.join(os.path.dirname(torch.__file__), "lib")
         path = os.path.join(lib_dir, "librccl.so")
-        self.lib = lib = ctypes.CDLL(path if os.path.exists(path) else "librccl.so")
+        try:
+            lib = ctypes.CDLL(path if os.path.exists(path) else "librccl.so")
+        except OSError:
+            lib = None
+        if not agree(lib is not None, group, device):
+            raise RuntimeError("librccl.so did not load on every rank")
+        self.lib = lib
         lib.ncclGetUniqueId.argtypes = [ctypes.POINTER(self._UniqueId)]
         lib.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, self._UniqueId, ctypes.c_int]
         lib.ncclAllGather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
@@ -95,15 +113,21 @@ class _RcclAllGather:
         lib.ncclGetErrorString.restype = ctypes.c_char_p
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         uid = self._UniqueId()
-        if rank == 0:
-            self._check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        box = [bytes(uid) if rank == 0 else None]  # the raw 128 bytes (the field reads up to a NUL)
+        box = [None]
+        if rank == 0 and lib.ncclGetUniqueId(ctypes.byref(uid)) == 0:
+            box = [bytes(uid)]  # the raw 128 bytes (the field itself reads up to a NUL)
         src = 0 if group is None else dist.get_global_rank(group, 0)
         dist.broadcast_object_list(box, src=src, group=group, device=device)
+        if box[0] is None:  # every rank sees the same box
+            raise RuntimeError("ncclGetUniqueId failed on rank 0")
         uid = self._UniqueId.from_buffer_copy(box[0])
-        self.comm = ctypes.c_void_p()
         with torch.cuda.device(device):
-            self._check(lib.ncclCommInitRank(ctypes.byref(self.comm), world, uid, rank), "ncclCommInitRank")
+            rc = lib.ncclCommInitRank(ctypes.byref(self.comm), world, uid, rank)
+            if not agree(rc == 0, group, device):
+                if rc == 0:
+                    lib.ncclCommDestroy(self.comm)
+                self.comm = ctypes.c_void_p()
+                raise RuntimeError(f"ncclCommInitRank failed on some rank (here: {rc})")
             self.stream = torch.cuda.Stream(device)  # from torch's pool: non-blocking
         hip = nat.hip_runtime()
         hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
@@ -185,7 +209,11 @@ class EpisodeReturnGather:
         self._rccl = None
         if self.collective and self.device.type == "cuda" and dist.get_backend(group) == "nccl" \
                 and os.environ.get("SCG_GATHER", "rccl") != "torch":
-            self._rccl = _RcclAllGather(group, self.device)
+            try:  # every rank takes the same branch (agree() inside)
+                self._rccl = _RcclAllGather(group, self.device)
+            except RuntimeError as exc:
+                import warnings
+                warnings.warn(f"episode-return gather falls back to dist.all_gather_into_tensor: {exc}")
         self.gathers = 0
 
     def on_episode_end(self, final_return):

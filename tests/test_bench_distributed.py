@@ -263,7 +263,8 @@ def _barrier_worker(rank, world, port, q, arr, iters):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import bench
-        bar = bench.NodeBarrier(rank, world, dist.barrier, timeout_s=120)
+        from gym_supplychain_amd.distributed import agree
+        bar = bench.NodeBarrier(rank, world, agree, timeout_s=120)
         bad = 0
         for i in range(iters):
             arr[rank] = i
@@ -295,3 +296,43 @@ def test_node_barrier_holds_every_rank(world):
         assert p.exitcode == 0
     assert all(v == 0 for v in res.values())
     assert set(glob.glob("/dev/shm/scg_bench_barrier_*")) <= before
+
+
+def _barrier_fail_worker(rank, world, port, q, fail_rank):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from gym_supplychain_amd.distributed import agree
+        if rank == fail_rank:  # this rank cannot map the page
+            real_open = os.open
+
+            def failing_open(path, *a, **k):
+                if str(path).startswith("/dev/shm/scg_bench_barrier_") and not (a and a[0] & os.O_CREAT):
+                    raise PermissionError("simulated")
+                return real_open(path, *a, **k)
+            os.open = failing_open
+        try:
+            bench.NodeBarrier(rank, world, agree, timeout_s=30)
+            q.put((rank, "built"))
+        except OSError:
+            q.put((rank, "raised"))
+        dist.barrier()  # no rank was left inside a collective
+    finally:
+        dist.destroy_process_group()
+
+
+def test_node_barrier_setup_fails_on_every_rank_together():
+    """One rank that cannot map the barrier page makes every rank raise (and fall back to
+    dist.barrier in GpuPlatform) instead of leaving the others in a collective."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_barrier_fail_worker, args=(r, 3, port, q, 2)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert set(res.values()) == {"raised"}
