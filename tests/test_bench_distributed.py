@@ -128,6 +128,10 @@ class CpuPlatform:
         self.world, self.rank, self.device = world, rank, "cpu"
         self.collectives = world > 1 if collectives is None else collectives
         self._base = bench.Platform()
+        self._bar = None
+        if self.collectives:  # the GPU platform's barrier (a shared page of the node)
+            from gym_supplychain_amd.distributed import agree
+            self._bar = bench.NodeBarrier(rank, world, agree, timeout_s=120)
 
     def make_env(self, n_envs, env_offset):
         self.env = StampedBatch(n_envs, env_offset)
@@ -140,7 +144,7 @@ class CpuPlatform:
         pass
 
     def barrier(self):
-        dist.barrier()
+        self._bar()
 
     def new_event(self):
         return _Stamp()
