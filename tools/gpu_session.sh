@@ -5,7 +5,9 @@
 # each) of the BeerGame step kernel and of each SupplyChain scenario's auto kernel. Every GPU
 # step has its own time limit; any failure stops the script.
 #   tools/gpu_session.sh TAG [STEPS]
-#   STEPS: comma list of tests,smoke,bench,sc,led,sweep,prof,pmc,scpmc (default all)
+#   STEPS: comma list of tests,smoke,bench,pg,sc,led,sweep,prof,pmc,scpmc (default all)
+#   pg: bench.py at one rank under torch.distributed.run with SCG_BENCH_PG=1 (the RCCL group,
+#   node barrier and return all-gather of the multi-GPU flow)
 # PMC summaries (here, after the pull):
 #   python tools/pmc_summary.py gpurun_out/pmc_TAG --meta bench=beergame-v0 n_envs=65536 --family bg
 #   python tools/pmc_summary.py gpurun_out/scpmc_TAG/SCN --meta bench=bench_sc scenario=SCN n_envs=N \
@@ -14,7 +16,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 TAG=${1:-r04}
-STEPS=",${2:-tests,smoke,bench,sc,led,sweep,prof,pmc,scpmc},"
+STEPS=",${2:-tests,smoke,bench,pg,sc,led,sweep,prof,pmc,scpmc},"
 mkdir -p "$OUT"
 stop() { echo "step '$1' ended with $2: stopping"; exit "$2"; }
 want() { [[ "$STEPS" == *",$1,"* ]]; }
@@ -31,6 +33,8 @@ want tests && run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeou
 want smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 want bench && run bench 400 python bench.py
 want bench && run bench_driver 300 python bench.py --steps 20 --warmup 5
+want pg && run bench_pg 300 env SCG_BENCH_PG=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 want sc && run bench_sc 900 python tools/bench_sc.py --scenario all --kernel auto
 want led && run bench_sc_ledgers 600 python tools/bench_sc.py --scenario both --kernel auto --build-info --no-cpu-baseline
 want sweep && run sweep_bg 600 python tools/sweep_bg.py --max-log2 24
