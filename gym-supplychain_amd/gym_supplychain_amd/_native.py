@@ -336,6 +336,10 @@ class MappedWord:
     def value(self, v):
         self._word.value = int(v)
 
+    @value.setter
+    def value(self, v):
+        self._word.value = int(v)
+
     def __del__(self):
         try:
             self._hip.hipHostFree(ctypes.c_void_p(self.host))

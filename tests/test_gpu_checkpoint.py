@@ -1,0 +1,151 @@
+"""Checkpoint / resume of the device vec envs (gym_supplychain_amd/checkpoint.py).
+
+A run is stepped, checkpointed mid-episode (through torch.save / torch.load with
+weights_only=True) and continued; a second env of the same configuration — different seed,
+different kernel where the chain allows — loads the checkpoint and is stepped with the same
+actions across auto-resets. Every output and every state buffer must match bit for bit,
+which also pins the continuation to the uninterrupted run (and so to the oracle the other
+GPU tests hold that run to).
+"""
+import io
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _roundtrip(sd):
+    buf = io.BytesIO()
+    torch.save(sd, buf)
+    buf.seek(0)
+    return torch.load(buf, map_location=DEV, weights_only=True)
+
+
+def _same(a, b, what):
+    if isinstance(a, torch.Tensor):
+        assert a.dtype == b.dtype and a.shape == b.shape, what
+        if a.is_floating_point():  # bit-exact, NaN included
+            assert torch.equal(a.view(torch.int64 if a.element_size() == 8 else torch.int32),
+                               b.view(torch.int64 if b.element_size() == 8 else torch.int32)), what
+        else:
+            assert torch.equal(a, b), what
+    elif isinstance(a, dict):
+        assert a.keys() == b.keys(), what
+        for k in a:
+            _same(a[k], b[k], f"{what}.{k}")
+    elif isinstance(a, (list, tuple)):
+        assert len(a) == len(b), what
+        for i, (x, y) in enumerate(zip(a, b)):
+            _same(x, y, f"{what}[{i}]")
+    else:
+        assert a == b, what
+
+
+def _continue(env, acts):
+    out = []
+    for a in acts:
+        obs, rew, done, info = env.step(a)
+        rec = {"obs": obs.clone(), "rew": rew.clone(), "done": done.clone()}
+        for k in ("terminal_observation", "episode_return"):
+            if k in info:
+                rec[k] = info[k].clone()
+        out.append(rec)
+    return out
+
+
+@pytest.mark.parametrize("demand,slab", [("poisson", True), ("poisson", False), ("fixed", True)])
+def test_beergame_resume_is_bit_exact(demand, slab):
+    from gym_supplychain_amd import BeerGameVecEnv
+    N, L = 640, 4
+    kw = dict(demand=demand, device=DEV, track_history=True, state_slab=slab)
+    a = BeerGameVecEnv(N, seed=11, **kw)
+    a.reset()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    acts = [torch.randint(0, 9, (N, L), generator=g, device=DEV, dtype=torch.int32) for _ in range(80)]
+    _continue(a, acts[:13])
+    sd = _roundtrip(a.state_dict())
+    assert sd["counters"]["week"] == 13
+    want = _continue(a, acts[13:])
+    b = BeerGameVecEnv(N, seed=999, **kw)  # another key: the checkpoint's must win
+    b.reset()
+    b.load_state_dict(sd)
+    assert (b.week, b.episode, b.seed_value) == (13, 0, 11)
+    got = _continue(b, acts[13:])
+    _same(want, got, "outputs")
+    _same(a.state_dict()["tensors"], b.state_dict()["tensors"], "state")
+    assert (a.week, a.episode) == (b.week, b.episode)
+    b.check_errors()
+
+
+def test_beergame2_resume_with_random_delays():
+    from gym_supplychain_amd import BeerGame2VecEnv
+    N = 256
+    kw = dict(customer_demand=(0, 12), shipment_delays=(1, 4), device=DEV)
+    a = BeerGame2VecEnv(N, seed=5, **kw)
+    a.reset()
+    g = torch.Generator(device=DEV).manual_seed(8)
+    acts = [torch.randint(0, 30, (N, 4), generator=g, device=DEV, dtype=torch.int32) for _ in range(60)]
+    _continue(a, acts[:20])
+    sd = _roundtrip(a.state_dict())
+    want = _continue(a, acts[20:])
+    b = BeerGame2VecEnv(N, seed=6, **kw)
+    b.load_state_dict(sd)
+    _same(want, _continue(b, acts[20:]), "outputs")
+    _same(a.state_dict()["tensors"], b.state_dict()["tensors"], "state")
+
+
+@pytest.mark.parametrize("src,dst", [("nodes", "staged"), ("staged", "lane"), ("lane", "nodes")])
+def test_supplychain_resume_across_kernels(src, dst):
+    """The heaps are saved env-major, so a checkpoint taken under one kernel's layout
+    resumes under another's (stochastic lead times, ledgers, auto-reset)."""
+    from gym_supplychain_amd import SupplyChainVecEnv
+    from gym_supplychain_amd.envs.scenarios import two_per_stage_nodes
+    nodes, kw = two_per_stage_nodes(total_time_steps=9, stochastic_leadtimes=True, avg_leadtime=2, max_leadtime=4,
+                                    build_info=True)
+    kw.pop("seed")
+    N = 300
+
+    def make(kernel, seed):
+        return SupplyChainVecEnv(N, nodes, seed=seed, device=DEV, obs_dtype=torch.float64, kernel=kernel, **kw)
+
+    a = make(src, 21)
+    a.reset()
+    g = torch.Generator(device=DEV).manual_seed(4)
+    acts = [torch.rand((N, a.n_actions), generator=g, device=DEV) * 2.2 - 1.1 for _ in range(25)]
+    _continue(a, acts[:5])
+    sd = _roundtrip(a.state_dict())
+    want = _continue(a, acts[5:])
+    b = make(dst, 22)
+    b.reset()
+    b.load_state_dict(sd)
+    assert (b.time_step, b.episode) == (5, 0)
+    _same(want, _continue(b, acts[5:]), "outputs")
+    sa, sb = a.state_dict()["tensors"], b.state_dict()["tensors"]
+    # heap slots past a heap's size are dead, and each kernel leaves its own values there
+    live = torch.arange(sa["heap_tk"].shape[2], device=DEV).view(1, 1, -1) < sa["heap_size"].unsqueeze(2)
+    for k in ("heap_tk", "heap_val"):
+        sa[k], sb[k] = torch.where(live, sa[k], 0), torch.where(live, sb[k], 0)
+    _same(sa, sb, "state")
+    for n in (0, 177, N - 1):
+        assert a.sc_episode(n) == b.sc_episode(n)
+    b.check_errors()
+
+
+def test_checkpoint_mismatches_are_refused():
+    from gym_supplychain_amd import BeerGameVecEnv, SupplyChainVecEnv
+    from gym_supplychain_amd.envs.scenarios import two_per_stage_nodes
+    a = BeerGameVecEnv(64, demand="poisson", device=DEV)
+    a.reset()
+    sd = a.state_dict()
+    with pytest.raises(ValueError, match="configuration"):
+        BeerGameVecEnv(64, demand="poisson", device=DEV, env_init_info={"inv_cost": 3}).load_state_dict(sd)
+    with pytest.raises(ValueError, match="configuration"):
+        BeerGameVecEnv(128, demand="poisson", device=DEV).load_state_dict(sd)
+    with pytest.raises(ValueError, match="buffers"):
+        BeerGameVecEnv(64, demand="poisson", device=DEV, track_history=True).load_state_dict(sd)
+    nodes, kw = two_per_stage_nodes(total_time_steps=9)
+    kw.pop("seed")
+    with pytest.raises(ValueError, match="BeerGameVecEnv"):
+        SupplyChainVecEnv(64, nodes, device=DEV, **kw).load_state_dict(sd)
