@@ -88,6 +88,12 @@ struct TileWalk {
   }
 };
 
+// Ledger reduce right after each wave's heaps phase (1) or after the last barrier (0, the
+// round-3 placement; A/B in DESIGN §6.7).
+#ifndef SCG_NODES_LED_EARLY
+#define SCG_NODES_LED_EARLY 1
+#endif
+
 #ifndef SCG_NODES_WPE
 #define SCG_NODES_WPE 4
 #endif
@@ -215,13 +221,53 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
     }
   NSTAMP(3);
 
-  // reward
+  // ledgers: entry q of an env, the nodes' entries added in node order (:750-760); at an
+  // auto-reset the finished episode's ledger is kept and the new one starts at int 0
   const bool terminal = a.flags & 1;
   const bool autoreset = a.flags & 2;
+  auto ledger_put = [&](int q, double lv, int32_t lk) {
+    const int64_t at = q * a.n + n;
+    if (autoreset) {
+      if (a.led_fv) {
+        a.led_fv[at] = lv;
+        a.led_fk[at] = lk;
+      }
+      lv = 0.0;
+      lk = np_kind_abi(NK_INT);
+    }
+    a.led_v[at] = lv;
+    a.led_k[at] = lk;
+  };
+  // entries first, first + step, ... of an env, two at a time (their loads in flight together)
+  auto ledger_entries = [&](int first, int step) {
+    const int nq = 2 * SCG_SC_LEDGER_KEYS * P;
+    for (int q0 = first; q0 < nq; q0 += 2 * step) {
+      const int q1 = q0 + step < nq ? q0 + step : -1;
+      const int64_t at0 = q0 * a.n + n, at1 = (q1 >= 0 ? q1 : q0) * a.n + n;
+      double lv0 = a.led_v[at0], lv1 = a.led_v[at1];
+      int32_t lk0 = a.led_k[at0], lk1 = a.led_k[at1];
+      sc_ledger_reduce_pair(c, q0, q1, a.ledp_v + n, a.n, lword + lane, 64, lv0, lk0, lv1, lk1);
+      ledger_put(q0, lv0, lk0);
+      if (q1 >= 0) ledger_put(q1, lv1, lk1);
+    }
+  };
+#if SCG_NODES_LED_EARLY
+  // Every slot and mark of an acted env is in place since the act barrier, so each wave
+  // reduces its share of the entries as soon as its heaps are done: the slot loads overlap
+  // the other waves' heaps and wave 0's reward instead of forming a phase of their own after
+  // the last barrier. A flagged env's slots are written by wave 0's serial walk below, which
+  // then reduces that env's entries itself.
+  if (ledgers && live && !flagged) ledger_entries(w, W);
+#endif
+
+  // reward
   if (w == 0 && live) {
     double reward;
     if (flagged) {  // untouched by act and heaps: the serial walk on its staged heaps
       reward = sc_nodes_serial<MAXD>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
+#if SCG_NODES_LED_EARLY
+      if (ledgers) ledger_entries(0, 1);
+#endif
     } else {
       Num total = pyint(0);
       for (int i = 0; i < NN; ++i) total = np_add(total, Num{cost_v[i * 64 + lane], cost_k[i * 64 + lane]});
@@ -239,25 +285,9 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   __syncthreads();
   NSTAMP(7);
 
-  // ledgers: entry q of every env, the nodes' entries added in node order (:750-760); at an
-  // auto-reset the finished episode's ledger is kept and the new one starts at int 0
-  if (ledgers && live)
-    for (int q = w; q < 2 * SCG_SC_LEDGER_KEYS * P; q += W) {
-      const int64_t at = q * a.n + n;
-      double lv = a.led_v[at];
-      int32_t lk = a.led_k[at];
-      sc_ledger_reduce(c, q, a.ledp_v + n, a.n, lword + lane, 64, lv, lk);
-      if (autoreset) {
-        if (a.led_fv) {
-          a.led_fv[at] = lv;
-          a.led_fk[at] = lk;
-        }
-        lv = 0.0;
-        lk = np_kind_abi(NK_INT);
-      }
-      a.led_v[at] = lv;
-      a.led_k[at] = lk;
-    }
+#if !SCG_NODES_LED_EARLY
+  if (ledgers && live) ledger_entries(w, W);
+#endif
 
   // out: the tile is this step's observation — obs, or the terminal observation when the
   // env resets now (then wave 0 writes the reset observation to obs), or both

@@ -103,7 +103,7 @@ struct ScEnv {
   // set, sc_note stores the value of node led_node's entry in its own slot ((node * 2 + part)
   // * 8 + key) * P + p of led_v, and marks it, with its NumPy type, in the node's per-product
   // word led_word[(node * P + p) * led_word_stride] (bit pk = part * 8 + key, the type in
-  // bits 16 + 3 pk ..); sc_ledger_reduce adds the marked slots to the ledger in node order
+  // bits 16 + 3 pk ..); sc_ledger_reduce(_pair) adds the marked slots to the ledger in node order
   // afterwards, as _update_statistics does (:750-760).
   int32_t led_node = 0;
   uint64_t* led_word = nullptr;
@@ -151,29 +151,53 @@ __host__ __device__ __forceinline__ void sc_led_begin_node(const ScCtx& c, ScEnv
   for (int p = 0; p < c.P; ++p) e.led_word[(static_cast<int64_t>(node) * c.P + p) * e.led_word_stride] = 0;
 }
 
-// Ledger entry q = (part * 8 + key) * P + p of one env after the step: the nodes' marked
-// entries added in node order (:750-760) to (lv, lk). cv: the slot values (stride cstride);
-// words: the per-(node, product) marks and types (stride wstride). The slots of a batch of
-// nodes are requested together, so the chain of adds waits on memory once per batch.
-__host__ __device__ inline void sc_ledger_reduce(const ScCtx& c, int q, const double* cv, int64_t cstride,
-                                                 const uint64_t* words, int64_t wstride, double& lv, int32_t& lk) {
-  const int p = q % c.P, pk = q / c.P;  // pk = part * 8 + key
+// Ledger entries q0 and q1 (q = (part * 8 + key) * P + p; q1 < 0: q0 alone) of one env after
+// the step: the nodes' marked entries added in node order (:750-760) to (lv, lk). cv: the
+// slot values (stride cstride); words: the per-(node, product) marks and types (stride
+// wstride). The slots of a batch of nodes are requested together for both entries, so the
+// two chains of adds wait on memory once per batch, not once per batch and entry.
+__host__ __device__ inline void sc_ledger_reduce_pair(const ScCtx& c, int q0, int q1, const double* cv,
+                                                      int64_t cstride, const uint64_t* words, int64_t wstride,
+                                                      double& lv0, int32_t& lk0, double& lv1, int32_t& lk1) {
+  const bool two = q1 >= 0;
+  const int p0 = q0 % c.P, pk0 = q0 / c.P;        // pk = part * 8 + key
+  const int p1 = two ? q1 % c.P : p0, pk1 = two ? q1 / c.P : pk0;
   constexpr int kBatch = 8;
-  Num acc{lv, np_kind_int(lk)};
+  Num acc0{lv0, np_kind_int(lk0)}, acc1{lv1, np_kind_int(lk1)};
+  auto slot = [&](int i, int pk, int p) { return ((static_cast<int64_t>(i) * 2 * SCG_SC_LEDGER_KEYS + pk) * c.P + p) * cstride; };
   for (int i0 = 0; i0 < c.n_nodes; i0 += kBatch) {
-    double v[kBatch];
+    double v0[kBatch], v1[kBatch];
 #pragma unroll
     for (int u = 0; u < kBatch; ++u)
-      if (i0 + u < c.n_nodes) v[u] = cv[((static_cast<int64_t>(i0 + u) * 2 * SCG_SC_LEDGER_KEYS + pk) * c.P + p) * cstride];
+      if (i0 + u < c.n_nodes) {
+        v0[u] = cv[slot(i0 + u, pk0, p0)];
+        v1[u] = two ? cv[slot(i0 + u, pk1, p1)] : 0.0;
+      }
 #pragma unroll
     for (int u = 0; u < kBatch; ++u) {
       if (i0 + u >= c.n_nodes) break;
-      const uint64_t w = words[(static_cast<int64_t>(i0 + u) * c.P + p) * wstride];
-      if ((w >> pk) & 1) acc = np_add(acc, Num{v[u], np_kind_int(static_cast<int>((w >> (16 + 3 * pk)) & 7))});
+      const uint64_t w0 = words[(static_cast<int64_t>(i0 + u) * c.P + p0) * wstride];
+      if ((w0 >> pk0) & 1) acc0 = np_add(acc0, Num{v0[u], np_kind_int(static_cast<int>((w0 >> (16 + 3 * pk0)) & 7))});
+      if (two) {
+        const uint64_t w1 = words[(static_cast<int64_t>(i0 + u) * c.P + p1) * wstride];
+        if ((w1 >> pk1) & 1) acc1 = np_add(acc1, Num{v1[u], np_kind_int(static_cast<int>((w1 >> (16 + 3 * pk1)) & 7))});
+      }
     }
   }
-  lv = acc.v;
-  lk = np_kind_abi(acc.k);
+  lv0 = acc0.v;
+  lk0 = np_kind_abi(acc0.k);
+  if (two) {
+    lv1 = acc1.v;
+    lk1 = np_kind_abi(acc1.k);
+  }
+}
+
+// One entry (sc_ledger_reduce_pair without the second).
+__host__ __device__ inline void sc_ledger_reduce(const ScCtx& c, int q, const double* cv, int64_t cstride,
+                                                 const uint64_t* words, int64_t wstride, double& lv, int32_t& lk) {
+  double lv1 = 0.0;
+  int32_t lk1 = 0;
+  sc_ledger_reduce_pair(c, q, -1, cv, cstride, words, wstride, lv, lk, lv1, lk1);
 }
 
 // est_episode at reset (:684-695): every entry the Python int 0

@@ -132,7 +132,14 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
       }
       auto reduce_ledger = [&]() {
         if (!ledger) return;
-        for (int q = 0; q < LQ; ++q) scg::sc_ledger_reduce(c, q, part_v.data(), 1, marks.data(), 1, led_v[q], led_k[q]);
+        // in pairs, as the kernel's waves take them (q, q + 1 here; q + W there)
+        for (int q = 0; q < LQ; q += 2) {
+          const int q1 = q + 1 < LQ ? q + 1 : -1;
+          double dv = 0.0;
+          int32_t dk = 0;
+          scg::sc_ledger_reduce_pair(c, q, q1, part_v.data(), 1, marks.data(), 1, led_v[q], led_k[q],
+                                     q1 >= 0 ? led_v[q1] : dv, q1 >= 0 ? led_k[q1] : dk);
+        }
         std::memcpy(ledger + static_cast<int64_t>(t - 1) * LQ, led_v.data(), sizeof(double) * LQ);
         std::memcpy(ledger_kind + static_cast<int64_t>(t - 1) * LQ, led_k.data(), sizeof(int32_t) * LQ);
       };

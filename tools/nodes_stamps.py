@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--dump", default="", help="also save every wave's stamps to DUMP_<step>.npz")
+    ap.add_argument("--build-info", action="store_true",
+                    help="the ledger instantiation (its reduce falls in the 'out' phase: stamps 7 -> 4)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -34,7 +36,7 @@ def main():
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda", 0)
     env = gsa.make_vec("sc-2perstage-v0", a.envs, seed=0, device=dev, obs_dtype=torch.float32, auto_reset=True,
-                       kernel="nodes")
+                       kernel="nodes", build_info=a.build_info)
     W = env._cfg.group
     waves = (a.envs + 63) // 64 * W
     env.reset()
@@ -51,7 +53,7 @@ def main():
         st = buf.astype(np.int64)
         t0 = st[:, 0].min()
         rel = st[:, :8] - t0
-        out = {"step": s, "waves": int(len(st)), "span": int(rel[:, 4].max()),
+        out = {"step": s, "build_info": a.build_info, "waves": int(len(st)), "span": int(rel[:, 4].max()),
                "start_p50_p90_max": [int(np.percentile(rel[:, 0], q)) for q in (50, 90, 100)],
                "end_p10_p50_max": [int(np.percentile(rel[:, 4], q)) for q in (10, 50, 100)]}
         names = ["stage", "barrier0", "act", "barrier1", "heaps", "reward+barrier2", "out", "whole"]
