@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--rev", default=None, help="take every csrc file and include/scgpu.h from this revision")
     ap.add_argument("--file", action="append", default=[], help="csrc/FILE=REV: one file from a revision")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--xflag", action="append", default=[],
+                    help="an extra compiler flag for every source (e.g. --xflag=-mllvm "
+                         "--xflag=-amdgpu-sched-strategy=max-ilp); disables --reuse-objs")
     ap.add_argument("--replace", nargs=3, action="append", default=[], metavar=("FILE", "OLD", "NEW"),
                     help="csrc/FILE: replace the exact text OLD by NEW (it must occur); for ablations")
     ap.add_argument("--reuse-objs", action="store_true",
@@ -76,7 +79,7 @@ def main():
                         ignore=shutil.ignore_patterns("*.so", "__pycache__"))
     out = os.path.join(pkg, "libscgpu.so")
     srcs = [os.path.join(csrc, s) for s in build_native.SOURCES]
-    if a.reuse_objs:
+    if a.reuse_objs and not a.xflag:
         tree_csrc, tree_objs = os.path.join(PKG, "csrc"), build_native.OUT + ".objs"
         same = lambda f: open(os.path.join(csrc, f)).read() == open(os.path.join(tree_csrc, f)).read()  # noqa: E731
         headers_same = all(same(f) for f in os.listdir(csrc) if f.endswith(".h")) and \
@@ -90,7 +93,8 @@ def main():
             fresh = os.path.exists(tobj) and os.path.getmtime(tobj) >= os.path.getmtime(os.path.join(tree_csrc, s_))
             if headers_same and same(s_) and fresh and not any(m in text for m in macros):
                 shutil.copyfile(os.path.join(tree_objs, obj), os.path.join(out + ".objs", obj))  # fresh mtime
-    build_native.compile_library(out, srcs, [inc, csrc], extra=[f"-D{d}" for d in a.defines], verbose=False)
+    build_native.compile_library(out, srcs, [inc, csrc], extra=[f"-D{d}" for d in a.defines] + a.xflag,
+                                 verbose=False)
     import sysconfig
     bout = os.path.join(pkg, "_scgpu_fast" + sysconfig.get_config_var("EXT_SUFFIX"))
     subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", sysconfig.get_paths()["include"], "-I", inc,
