@@ -96,4 +96,45 @@ __host__ __device__ __forceinline__ bool np_eq(Num a, Num b) {
 // Python's builtin min(a, b): b if b < a else a (keeps the chosen operand's kind).
 __host__ __device__ __forceinline__ Num py_min(Num a, Num b) { return np_lt(b, a) ? b : a; }
 
+// The same operations where the caller knows that no promoted kind in the region is float32
+// (kNo32: the operands are float64, Python or int64 scalars, or a float32 meeting a float64):
+// then each is the plain double operation with the promoted kind, and a comparison is the
+// exact one — one instruction where the kind-generic form computes both roundings and
+// selects. Identical values and kinds.
+template <bool kNo32>
+__host__ __device__ __forceinline__ Num np_add_k(Num a, Num b) {
+  if constexpr (kNo32) return Num{a.v + b.v, np_promote(a.k, b.k)};
+  return np_add(a, b);
+}
+template <bool kNo32>
+__host__ __device__ __forceinline__ Num np_sub_k(Num a, Num b) {
+  if constexpr (kNo32) return Num{a.v - b.v, np_promote(a.k, b.k)};
+  return np_sub(a, b);
+}
+template <bool kNo32>
+__host__ __device__ __forceinline__ Num np_mul_k(Num a, Num b) {
+  if constexpr (kNo32) return Num{a.v * b.v, np_promote(a.k, b.k)};
+  return np_mul(a, b);
+}
+template <bool kNo32>
+__host__ __device__ __forceinline__ Num np_div_k(Num a, Num b) {
+  if constexpr (kNo32) return Num{a.v / b.v, np_promote(a.k, b.k) | NK_PYF};
+  return np_div(a, b);
+}
+template <bool kNo32>
+__host__ __device__ __forceinline__ bool np_lt_k(Num a, Num b) {
+  if constexpr (kNo32) return a.v < b.v;
+  return np_lt(a, b);
+}
+
+// True when every active lane of the wave has `p` (the host build runs one env: p itself).
+// A kind test made wave-uniform this way picks one instantiation for the whole wave.
+__host__ __device__ __forceinline__ bool wave_all(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __all(p);
+#else
+  return p;
+#endif
+}
+
 }  // namespace scg

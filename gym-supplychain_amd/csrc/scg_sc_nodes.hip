@@ -200,7 +200,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   // act: every node at once (a node's act needs only what its own heaps release)
   if (go)
     for (int i = w; i < NN; i += W) {
-      const Num cst = sc_nodes_act<MAXD>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
+      const Num cst = sc_nodes_act<MAXD, !LED>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
       cost_v[i * 64 + lane] = cst.v;
       cost_k[i * 64 + lane] = cst.k;
       for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
@@ -264,7 +264,7 @@ void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
   if (w == 0 && live) {
     double reward;
     if (flagged) {  // untouched by act and heaps: the serial walk on its staged heaps
-      reward = sc_nodes_serial<MAXD>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
+      reward = sc_nodes_serial<MAXD, !LED>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
 #if SCG_NODES_LED_EARLY
       if (ledgers) ledger_entries(0, 1);
 #endif

@@ -241,7 +241,7 @@ void sc_step_staged_kernel(const ScArgs a) {
     if (node_obs) main(o, x);
     if (both) extra(o, x);
   };
-  const double reward = sc_staged_step<MAXD>(c, g, lh, in, a.act + n * c.A, a.t, sink);
+  const double reward = sc_staged_step<MAXD, !LED>(c, g, lh, in, a.act + n * c.A, a.t, sink);
   a.rew[n] = reward;
   if (a.ep_ret) {
     const double r = a.ep_ret[n] + reward;

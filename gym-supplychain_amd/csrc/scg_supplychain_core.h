@@ -9,6 +9,8 @@
 // functions over env-fastest SoA arrays.
 #pragma once
 
+#include <type_traits>
+
 #include <stdint.h>
 
 #include "scg_const.h"
@@ -382,7 +384,7 @@ struct NumVec {
 // Sorting (value, index) tuples is done by ranks so every array index is a compile-time
 // constant (MAXD-unrolled loops): the arrays stay in registers instead of scratch. K <= MAXD
 // bounds the loops (a node with D <= K destinations runs the K-sized split; D is uniform).
-template <int MAXD, int K = MAXD>
+template <int MAXD, int K = MAXD, bool kNo32 = false>
 __host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num limit, NumVec<MAXD>& out) {
 #pragma unroll
   for (int i = 0; i < MAXD; ++i) out.set(i, pyint(0));
@@ -411,12 +413,12 @@ __host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num l
     for (int i = 0; i < K; ++i)
       if (i < D && rank[i] == s) v = vals[i];
     const Num diff = first ? np_sub(Num{v, NK_F32}, pyint(0)) : np_sub(Num{v, NK_F32}, Num{prev, NK_F32});
-    Num amt = np_mul(diff, limit);
-    if (np_lt(left, amt)) amt = left;
+    Num amt = np_mul_k<kNo32>(diff, limit);  // kNo32: a float64 limit, so a float64 amount
+    if (np_lt_k<kNo32>(left, amt)) amt = left;
 #pragma unroll
     for (int i = 0; i < K; ++i)
       if (i < D && rank[i] == s) out.set(i, amt);
-    left = np_sub(left, amt);
+    left = np_sub_k<kNo32>(left, amt);
     prev = v;
     first = false;
   }
@@ -427,7 +429,7 @@ __host__ __device__ inline void sc_split(const float (&vals)[MAXD], int D, Num l
 // rank, the cut is walked in slot order, and amount s is left in slot s, where destination
 // i reads it at rank[i] — no O(D^2) selects and no per-destination amount registers.
 // Returns false when nothing is cut (limit <= 0: every amount is the Python int 0).
-template <int MAXD, class Scratch>
+template <int MAXD, bool kNo32 = false, class Scratch>
 __host__ __device__ inline bool sc_split_scratch(const float (&vals)[MAXD], int D, Num limit, const Scratch& scr,
                                                  int (&rank)[MAXD]) {
   Num left = limit;
@@ -450,10 +452,10 @@ __host__ __device__ inline bool sc_split_scratch(const float (&vals)[MAXD], int 
   for (int s = 0; s < D; ++s) {
     const float v = scr.scratch_value(s);
     const Num diff = s == 0 ? np_sub(Num{v, NK_F32}, pyint(0)) : np_sub(Num{v, NK_F32}, Num{prev, NK_F32});
-    Num amt = np_mul(diff, limit);
-    if (np_lt(left, amt)) amt = left;
+    Num amt = np_mul_k<kNo32>(diff, limit);
+    if (np_lt_k<kNo32>(left, amt)) amt = left;
     scr.scratch_put(s, amt);
-    left = np_sub(left, amt);
+    left = np_sub_k<kNo32>(left, amt);
     prev = v;
   }
   return true;
@@ -461,15 +463,15 @@ __host__ __device__ inline bool sc_split_scratch(const float (&vals)[MAXD], int 
 
 // The split sized to the node: chains mixing narrow and wide nodes (ntom: 8 and 16
 // destinations) run the narrow nodes' O(D^2) ranking at their own size.
-template <int MAXD>
+template <int MAXD, bool kNo32 = false>
 __host__ __device__ __forceinline__ void sc_split_d(const float (&vals)[MAXD], int D, Num limit, NumVec<MAXD>& out) {
   if constexpr (MAXD > 8) {
     if (D <= 8) {
-      sc_split<MAXD, 8>(vals, D, limit, out);
+      sc_split<MAXD, 8, kNo32>(vals, D, limit, out);
       return;
     }
   }
-  sc_split<MAXD>(vals, D, limit, out);
+  sc_split<MAXD, MAXD, kNo32>(vals, D, limit, out);
 }
 
 // Action k of this env, denormalised like _denormalize_action (:697-698): (a + 1) / 2 on
@@ -516,12 +518,15 @@ __host__ __device__ __forceinline__ double sc_receive(const HV& h, int32_t& sz, 
 
 // SC_Node.act (:208-396) for node `ni` at time t; `act` = this env's raw float32 action
 // row. Returns the node's cost with its NumPy kind. MAXD bounds the node's destinations.
+// kKindPaths: the ship part also has a plain double instantiation for waves whose kinds
+// never round to float32 (below); on in the staged and node-parallel kernels without
+// ledgers, off where its registers or code size would cost occupancy or inlining.
 // kHeapsDone: the caller already did this node's heap work — the receive pops with their
 // stock update and the SUPPLY pushes (sc_staged_heap) — so act touches no heap of its own;
 // a node's heaps are independent of everything else act computes, so only the order of
 // operations on each heap has to be the reference's, and it is.
-template <int MAXD, class Push = DirectPush, bool kHeapsDone = false>
-__host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& ltc, WordCache& dmc, int ni,
+template <int MAXD, class Push = DirectPush, bool kHeapsDone = false, bool kKindPaths = false>
+__host__ __device__ __forceinline__ Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& ltc, WordCache& dmc, int ni,
                                            const float* act, int t, const Push& push = Push()) {
   ScNode& nd = c.nodes[ni];
   const int P = c.P;
@@ -578,74 +583,95 @@ __host__ __device__ inline Num sc_node_act(const ScCtx& c, ScEnv& e, WordCache& 
       Num over_ship = pyint(0), over_proc = pyint(0);
       const Num material = f64(sc_stock(c, e, ni, p));
       if (np_lt(pyint(0), material)) {
-        float vals[MAXD];
-        NumVec<MAXD> out;
-        int rank[MAXD];
-        bool cut = false;  // kLdsSplit: the split's amounts are in the scratch slots
-        sc_ship_vals<MAXD>(act, nd.action_offset + a_i, D, vals);
-        if constexpr (Push::kLdsSplit) {
-          cut = sc_split_scratch<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), push, rank);
-        } else {
-          sc_split_d<MAXD>(vals, D, py_min(pyint(nd.stock_capacity[p]), material), out);
-        }
-        SCG_ACCP(e.dbg, 9);
-        // The reference's per-destination passes — processing capacity and ratio
-        // (:298-310), ship capacity (:312-328), sum(amounts) (:331), the pushes (:344-348)
-        // and sum(calculate_costs(amounts_to_ship)) (:352) — each carry their own
-        // accumulator in destination order and read only destination i's values; the
-        // stock update between them (:332) touches none of them. So they run fused, one
-        // destination at a time, every accumulator seeing the reference's order, and no
-        // per-destination array besides the split's output stays live.
-        Num leaving = pyint(0), ship_cost = pyint(0), ship_units = pyint(0);
-        auto dest_step = [&](int i) {
-          Num o;
-          if constexpr (Push::kLdsSplit)
-            o = cut ? push.scratch_get(rank[i]) : pyint(0);
-          else
-            o = out.get_dyn(i);
-          Num snt = o;  // amounts_to_ship = amounts.copy() (:292)
-          if (factory) {
-            if (np_lt(pyint(0), o)) {
-              if (np_lt(proc_left, o)) {
-                over_proc = np_add(over_proc, np_sub(o, proc_left));
-                o = proc_left;
-              }
-              proc_left = np_sub(proc_left, o);
-            }
-            snt = np_div(o, pyint(nd.processing_ratio[p]));
-          }
-          const Num cap = ship_left.get_dyn(i);
-          if (np_lt(pyint(0), snt) && np_lt(cap, snt)) {
-            over_ship = np_add(over_ship, np_sub(snt, cap));
-            snt = cap;
-            o = factory ? np_mul(snt, pyint(nd.processing_ratio[p])) : snt;
-            ship_left.set_dyn(i, np_sub(cap, o));  // only on overflow, by the new amount
-          }
-          leaving = np_add(leaving, o);
-          if (np_lt(pyint(0), snt))
-            push.ship(c, e, ni, i, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
-          else if constexpr (Push::kClearInAct)
-            push.noship(c, ni, i, p);
-          ship_cost = np_add(ship_cost, np_mul(snt, pyint(nd.dest_costs[p][i])));
-          ship_units = np_add(ship_units, snt);  // sum(amounts_to_ship) (:356)
-        };
-        if constexpr (Push::kUnroll) {  // every index static: the NumVecs stay in registers
+        const Num limit = py_min(pyint(nd.stock_capacity[p]), material);  // :61-64
+        // The split and the per-destination passes below round to float32 only through a
+        // float32 amount, which comes from an int limit (float32 action * int, :56-57, 86), or
+        // through a float32 left in proc_left or ship_left by an earlier product. Without
+        // either (the stock is the limit, or nothing is cut) every promoted kind is float64 or
+        // a Python / int64 scalar, and the whole wave runs the plain double instantiation.
+        bool f32_left = proc_left.k == NK_F32;
 #pragma unroll
-          for (int i = 0; i < MAXD; ++i)
-            if (i < D) dest_step(i);
+        for (int j = 0; j < MAXD; ++j) f32_left |= ship_left.get(j).k == NK_F32;
+        const bool no32 = kKindPaths && wave_all(!f32_left && (limit.k != NK_INT || !np_lt(pyint(0), limit)));
+        auto ship_product = [&](auto no32_tag) __attribute__((always_inline)) {
+          constexpr bool kNo32 = decltype(no32_tag)::value;
+          float vals[MAXD];
+          NumVec<MAXD> out;
+          int rank[MAXD];
+          bool cut = false;  // kLdsSplit: the split's amounts are in the scratch slots
+          sc_ship_vals<MAXD>(act, nd.action_offset + a_i, D, vals);
+          if constexpr (Push::kLdsSplit) {
+            cut = sc_split_scratch<MAXD, kNo32>(vals, D, limit, push, rank);
+          } else {
+            sc_split_d<MAXD, kNo32>(vals, D, limit, out);
+          }
+          SCG_ACCP(e.dbg, 9);
+          // The reference's per-destination passes — processing capacity and ratio
+          // (:298-310), ship capacity (:312-328), sum(amounts) (:331), the pushes (:344-348)
+          // and sum(calculate_costs(amounts_to_ship)) (:352) — each carry their own
+          // accumulator in destination order and read only destination i's values; the
+          // stock update between them (:332) touches none of them. So they run fused, one
+          // destination at a time, every accumulator seeing the reference's order, and no
+          // per-destination array besides the split's output stays live.
+          Num leaving = pyint(0), ship_cost = pyint(0), ship_units = pyint(0);
+          auto dest_step = [&](int i) {
+            Num o;
+            if constexpr (Push::kLdsSplit)
+              o = cut ? push.scratch_get(rank[i]) : pyint(0);
+            else
+              o = out.get_dyn(i);
+            Num snt = o;  // amounts_to_ship = amounts.copy() (:292)
+            if (factory) {
+              if (np_lt_k<kNo32>(pyint(0), o)) {
+                if (np_lt_k<kNo32>(proc_left, o)) {
+                  over_proc = np_add_k<kNo32>(over_proc, np_sub_k<kNo32>(o, proc_left));
+                  o = proc_left;
+                }
+                proc_left = np_sub_k<kNo32>(proc_left, o);
+              }
+              snt = np_div_k<kNo32>(o, pyint(nd.processing_ratio[p]));
+            }
+            const Num cap = ship_left.get_dyn(i);
+            if (np_lt_k<kNo32>(pyint(0), snt) && np_lt_k<kNo32>(cap, snt)) {
+              over_ship = np_add_k<kNo32>(over_ship, np_sub_k<kNo32>(snt, cap));
+              snt = cap;
+              o = factory ? np_mul_k<kNo32>(snt, pyint(nd.processing_ratio[p])) : snt;
+              ship_left.set_dyn(i, np_sub_k<kNo32>(cap, o));  // only on overflow, by the new amount
+            }
+            leaving = np_add_k<kNo32>(leaving, o);
+            if (np_lt_k<kNo32>(pyint(0), snt))
+              push.ship(c, e, ni, i, nd.dests[i], p, t + node_leadtime(c, e, ltc, nd, t, lt_base + i), snt);
+            else if constexpr (Push::kClearInAct)
+              push.noship(c, ni, i, p);
+            ship_cost = np_add_k<kNo32>(ship_cost, np_mul_k<kNo32>(snt, pyint(nd.dest_costs[p][i])));
+            ship_units = np_add_k<kNo32>(ship_units, snt);  // sum(amounts_to_ship) (:356)
+          };
+          if constexpr (Push::kUnroll) {  // every index static: the NumVecs stay in registers
+#pragma unroll
+            for (int i = 0; i < MAXD; ++i)
+              if (i < D) dest_step(i);
+          } else {
+            for (int i = 0; i < D; ++i) dest_step(i);
+          }
+          SCG_ACCP(e.dbg, 10);
+          // float64 array element minus the promoted scalar (:332); nothing above wrote it
+          sc_stock(c, e, ni, p) = material.v - leaving.v;
+          if (factory) {
+            const Num proc = np_mul(leaving, pyint(nd.processing_cost[p]));
+            cost = np_add(cost, proc);
+            sc_note(c, e, LK_PROCESS, p, proc, leaving);
+          }
+          cost = np_add(cost, ship_cost);
+          sc_note(c, e, LK_SHIP, p, ship_cost, ship_units);
+        };
+        if constexpr (kKindPaths) {
+          if (no32)
+            ship_product(std::true_type{});
+          else
+            ship_product(std::false_type{});
         } else {
-          for (int i = 0; i < D; ++i) dest_step(i);
+          ship_product(std::false_type{});
         }
-        SCG_ACCP(e.dbg, 10);
-        // float64 array element minus the promoted scalar (:332); nothing above wrote it
-        sc_stock(c, e, ni, p) = material.v - leaving.v;
-        if (factory) {
-          const Num proc = np_mul(leaving, pyint(nd.processing_cost[p]));
-          cost = np_add(cost, proc);
-          sc_note(c, e, LK_PROCESS, p, proc, leaving);
-        }
-        cost = np_add(cost, ship_cost);
-        sc_note(c, e, LK_SHIP, p, ship_cost, ship_units);
       } else {
         if constexpr (Push::kClearInAct) push.noship_all(c, ni, p);
       }

@@ -137,7 +137,7 @@ __host__ __device__ inline bool sc_nodes_stage(const ScCtx& c, const ScEnv& g, c
 
 // act: node i receives (recv[p * rstride], from its stage) and acts; its heaps are not
 // touched, its shipments go to the inbox. Returns the node's cost with its NumPy kind.
-template <int MAXD>
+template <int MAXD, bool kKindPaths = false>
 __host__ __device__ inline Num sc_nodes_act(const ScCtx& c, ScEnv& g, const NodesInbox& in, const double* recv,
                                             int64_t rstride, const float* act, int t, int i) {
   for (int p = 0; p < c.P; ++p) {
@@ -147,7 +147,7 @@ __host__ __device__ inline Num sc_nodes_act(const ScCtx& c, ScEnv& g, const Node
   if (!c.nodes[i].last_level) in.clear(c, i);
   sc_led_begin_node(c, g, i);
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
-  return sc_node_act<MAXD, NodesInbox, true>(c, g, ltc, dmc, i, act, t, in);
+  return sc_node_act<MAXD, NodesInbox, true, kKindPaths>(c, g, ltc, dmc, i, act, t, in);
 }
 
 // heaps: everything heap (i, p), staged in `lh` with size sz, sees in step t, in the
@@ -192,7 +192,7 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
 // doing its heaps' work with the real pops — after the pushes earlier nodes made this step,
 // as the reference does — then the rest of its act (the staged kernel's order). Returns
 // the reward.
-template <int MAXD, class HeapAt, class Sink>
+template <int MAXD, bool kKindPaths = false, class HeapAt, class Sink>
 __host__ __device__ inline double sc_nodes_serial(const ScCtx& c, ScEnv& g, const HeapAt& heap_at, int32_t* sz,
                                                   int64_t sz_stride, const NodesInbox& in, const float* act, int t,
                                                   Sink& out) {
@@ -206,7 +206,7 @@ __host__ __device__ inline double sc_nodes_serial(const ScCtx& c, ScEnv& g, cons
     }
     if (!c.nodes[i].last_level) in.clear(c, i);
     sc_led_begin_node(c, g, i);
-    total = np_add(total, sc_node_act<MAXD, NodesInbox, true>(c, g, ltc, dmc, i, act, t, in));
+    total = np_add(total, sc_node_act<MAXD, NodesInbox, true, kKindPaths>(c, g, ltc, dmc, i, act, t, in));
     for (int p = 0; p < c.P; ++p) sc_observe_stock(c, g, i, p, out);
   }
   return np_neg(total).v;

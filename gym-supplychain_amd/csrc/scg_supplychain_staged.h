@@ -224,7 +224,7 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 // shares. out(o, x) receives the node observation elements (the caller adds the demand and
 // time-to-go ones). Returns the reward. (Staging the node's stocks in LDS as well measured
 // no faster on MI355X: stock accesses are few and cache-resident.)
-template <int MAXD, class Sink>
+template <int MAXD, bool kKindPaths = false, class Sink>
 __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView8& lh, const StagedInbox& in,
                                                  const float* act, int t, Sink& out) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
@@ -239,7 +239,7 @@ __host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const
     for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out, scg_acc_);
     if (!StagedInbox::kClearInAct && !nd.last_level) in.clear(c, i);
     SCG_ACC(7);
-    total = np_add(total, sc_node_act<MAXD, StagedInbox, true>(c, g, ltc, dmc, i, act, t, in));
+    total = np_add(total, sc_node_act<MAXD, StagedInbox, true, kKindPaths>(c, g, ltc, dmc, i, act, t, in));
     SCG_ACC(5);
     for (int p = 0; p < c.P; ++p) sc_observe_stock(c, g, i, p, out);
     SCG_ACC(6);

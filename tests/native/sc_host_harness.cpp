@@ -102,11 +102,11 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
       auto out = [row](int o, double v) { row[o] = v; };
       double r = 0.0;
       switch (scg::sc_maxd_bucket(cfg->max_dests)) {
-        case 2: r = scg::sc_staged_step<2>(c, et, loc, in, a, t, out); break;
-        case 4: r = scg::sc_staged_step<4>(c, et, loc, in, a, t, out); break;
-        case 8: r = scg::sc_staged_step<8>(c, et, loc, in, a, t, out); break;
-        case 16: r = scg::sc_staged_step<16>(c, et, loc, in, a, t, out); break;
-        default: r = scg::sc_staged_step<32>(c, et, loc, in, a, t, out); break;
+        case 2: r = scg::sc_staged_step<2, true>(c, et, loc, in, a, t, out); break;
+        case 4: r = scg::sc_staged_step<4, true>(c, et, loc, in, a, t, out); break;
+        case 8: r = scg::sc_staged_step<8, true>(c, et, loc, in, a, t, out); break;
+        case 16: r = scg::sc_staged_step<16, true>(c, et, loc, in, a, t, out); break;
+        default: r = scg::sc_staged_step<32, true>(c, et, loc, in, a, t, out); break;
       }
       rewards[t - 1] = r;
       for (int k = 0; k < c.R * c.P; ++k) scg::sc_observe_demand(c, et, t, k, out);
@@ -158,11 +158,11 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
         nodes_fallbacks += flagged ? 1 : 0;
         double r = 0.0;
         switch (scg::sc_maxd_bucket(cfg->max_dests)) {
-          case 2: r = scg::sc_nodes_serial<2>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
-          case 4: r = scg::sc_nodes_serial<4>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
-          case 8: r = scg::sc_nodes_serial<8>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
-          case 16: r = scg::sc_nodes_serial<16>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
-          default: r = scg::sc_nodes_serial<32>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          case 2: r = scg::sc_nodes_serial<2, true>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          case 4: r = scg::sc_nodes_serial<4, true>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          case 8: r = scg::sc_nodes_serial<8, true>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          case 16: r = scg::sc_nodes_serial<16, true>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
+          default: r = scg::sc_nodes_serial<32, true>(c, et, lheap, hsz.data(), 1, in, a, t, out); break;
         }
         rewards[t - 1] = r;
         for (int k = 0; k < c.R * c.P; ++k) scg::sc_observe_demand(c, et, t, k, out);
@@ -173,11 +173,11 @@ static int episode_impl(int mode, const scg_sc_config* cfg, const scg_sc_node* n
       }
       for (int i = c.n_nodes - 1; i >= 0; --i) {
         switch (scg::sc_maxd_bucket(cfg->max_dests)) {
-          case 2: cost[i] = scg::sc_nodes_act<2>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
-          case 4: cost[i] = scg::sc_nodes_act<4>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
-          case 8: cost[i] = scg::sc_nodes_act<8>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
-          case 16: cost[i] = scg::sc_nodes_act<16>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
-          default: cost[i] = scg::sc_nodes_act<32>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          case 2: cost[i] = scg::sc_nodes_act<2, true>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          case 4: cost[i] = scg::sc_nodes_act<4, true>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          case 8: cost[i] = scg::sc_nodes_act<8, true>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          case 16: cost[i] = scg::sc_nodes_act<16, true>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
+          default: cost[i] = scg::sc_nodes_act<32, true>(c, et, in, recv.data() + i * c.P, 1, a, t, i); break;
         }
         for (int p = 0; p < c.P; ++p) scg::sc_observe_stock(c, et, i, p, out);
       }
