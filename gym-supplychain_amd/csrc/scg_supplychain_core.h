@@ -318,6 +318,7 @@ __host__ __device__ __forceinline__ void sc_push(const ScCtx& c, ScEnv& e, int n
 struct DirectPush {
   static constexpr bool kUnroll = false;
   static constexpr bool kLdsSplit = false;  // see sc_split_scratch
+  static constexpr bool kVecActions = false;  // see sc_ship_vals
   static constexpr bool kClearInAct = false;  // see StagedInbox::noship
   __host__ __device__ Num scratch_get(int) const { return pyint(0); }
   __host__ __device__ void noship(const ScCtx&, int, int, int) const {}
@@ -494,8 +495,35 @@ __host__ __device__ __forceinline__ void sc_ship_vals_k(const float* raw, int ba
 #pragma unroll
   for (int i = 0; i < MAXD; ++i) vals[i] = (i < K && i < D) ? sc_denorm(x[i < K ? i : 0]) : 0.0f;
 }
-template <int MAXD>
+// Four destinations' actions per 16-byte load (global memory is dword-aligned here, which the
+// loads need), for nodes whose destination count is a multiple of four: an env-major action
+// row is one cache line apart per lane, so a quarter of the load instructions is a quarter of
+// the lines the vector memory pipeline looks up. Only chunks inside the node's actions are read.
+template <int MAXD, int K>
+__host__ __device__ __forceinline__ void sc_ship_vals_v4(const float* raw, int base, int D, float (&vals)[MAXD]) {
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  f4u x[K / 4];
+#pragma unroll
+  for (int j = 0; j < K / 4; ++j)
+    x[j] = 4 * j < D ? *reinterpret_cast<const f4u*>(raw + base + 4 * j) : f4u{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < MAXD; ++i) vals[i] = (i < K && i < D) ? sc_denorm(x[(i < K ? i : 0) / 4][i % 4]) : 0.0f;
+}
+
+template <int MAXD, bool kVec = false>
 __host__ __device__ __forceinline__ void sc_ship_vals(const float* raw, int base, int D, float (&vals)[MAXD]) {
+  if constexpr (kVec && MAXD >= 4) {
+    if ((D & 3) == 0) {
+      if constexpr (MAXD > 8) {
+        if (D <= 8) {
+          sc_ship_vals_v4<MAXD, 8>(raw, base, D, vals);
+          return;
+        }
+      }
+      sc_ship_vals_v4<MAXD, MAXD>(raw, base, D, vals);
+      return;
+    }
+  }
   if constexpr (MAXD > 8) {
     if (D <= 8) {
       sc_ship_vals_k<MAXD, 8>(raw, base, D, vals);
@@ -599,7 +627,7 @@ __host__ __device__ __forceinline__ Num sc_node_act(const ScCtx& c, ScEnv& e, Wo
           NumVec<MAXD> out;
           int rank[MAXD];
           bool cut = false;  // kLdsSplit: the split's amounts are in the scratch slots
-          sc_ship_vals<MAXD>(act, nd.action_offset + a_i, D, vals);
+          sc_ship_vals<MAXD, Push::kVecActions>(act, nd.action_offset + a_i, D, vals);
           if constexpr (Push::kLdsSplit) {
             cut = sc_split_scratch<MAXD, kNo32>(vals, D, limit, push, rank);
           } else {

@@ -42,6 +42,7 @@ struct LevelInbox {
 
   static constexpr bool kUnroll = true;  // an LDS store per destination
   static constexpr bool kLdsSplit = false;
+  static constexpr bool kVecActions = false;
   static constexpr bool kClearInAct = false;  // cleared before the act
   __host__ __device__ Num scratch_get(int) const { return pyint(0); }
   __host__ __device__ void noship(const ScCtx&, int, int, int) const {}

@@ -68,6 +68,7 @@ struct StagedInbox {
 
   static constexpr bool kUnroll = true;  // a store per destination
   static constexpr bool kLdsSplit = true;
+  static constexpr bool kVecActions = true;  // the env's action row in HBM
 #ifndef SCG_STAGED_NOSHIP
 #define SCG_STAGED_NOSHIP 1
 #endif
