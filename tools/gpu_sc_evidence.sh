@@ -1,6 +1,7 @@
+#!/bin/bash
 # Final-tree SupplyChain evidence in one call: PMC passes per scenario, their summaries
-# (tools/gpu_sc_evidence.sh TAG; run through gpurun)
 # (written to profiles/ for bench_sc's keyed lookup and copied to gpurun_out/), then bench_sc
+# with same-host CPU baselines and the ledger runs.   tools/gpu_sc_evidence.sh TAG (via gpurun)
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 TAG=${1:-r04zd}
 bash tools/gpu_session.sh ${TAG} scpmc || exit 1
