@@ -166,11 +166,11 @@ def cpu_worker_inputs(idx, n_episodes):
     return demands, acts
 
 
-def _cpu_worker(arg):
-    idx, budget_s = arg
+def _cpu_worker(idx, budget_s, start):
     sys.path.insert(0, REPO)
     from oracle.beergame import BeerGameOracle
     demands, acts = cpu_worker_inputs(idx, 64)
+    start()  # every worker's inputs are drawn: the timed part starts together
     steps, ep = 0, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:  # construct + reset + 35 steps per episode
@@ -184,22 +184,99 @@ def _cpu_worker(arg):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(budget_s=1.5, max_procs=16):
-    """Per-env NumPy restatement of BeerGameEnv.step on the host's cores (oracle, 'port')."""
-    import multiprocessing as mp
+def _cgroup_cpu_quota():
+    """CPUs this process group may use per the cgroup CPU quota (v2 cpu.max, v1 cfs), or None."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            quota = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            period = int(f.read())
+        return None if quota <= 0 else quota / period
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpus():
+    """The host CPUs a baseline may use: the CPU model (/proc/cpuinfo), the cores in this
+    process's affinity mask, the cgroup CPU quota if one is set, and the worker count: every
+    core of the affinity mask (P = os.cpu_count() processes), down to the quota
+    when one caps the job below it (processes past the quota would only share its CPU time)."""
+    import math
+    try:
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    procs = max(1, min(max_procs, cores))
+        affinity = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = _cgroup_cpu_quota()
+    procs = affinity if quota is None else max(1, min(affinity, math.ceil(quota)))
+    return {"cpu_model": model, "affinity_cores": affinity, "os_cpu_count": os.cpu_count(),
+            "cgroup_quota_cpus": quota, "procs": procs}
+
+
+def cpu_note(cpus):
+    """How the worker count was chosen, for the baseline's `sample` text."""
+    if cpus["procs"] < cpus["affinity_cores"]:
+        return (f"the job's cgroup CPU quota of {cpus['cgroup_quota_cpus']:g} CPUs caps it below the "
+                f"{cpus['affinity_cores']} cores of its affinity mask; {cpus['cpu_model']}")
+    return f"one per core of the affinity mask; {cpus['cpu_model']}"
+
+
+def _pool_entry(fn, idx, budget_s, barrier, q):
+    try:
+        q.put((idx, fn(idx, budget_s, lambda: barrier.wait(600))))
+    except BaseException as exc:  # a worker that fails must not leave the others at the barrier
+        barrier.abort()
+        q.put((idx, repr(exc)))
+
+
+def cpu_pool(fn, budget_s, procs):
+    """fn(idx, budget_s, start) -> (steps, wall s) on `procs` spawned processes (no GPU use;
+    each calls start() once its inputs are ready, so the timed parts overlap). Returns
+    (sum of steps / max of wall, sum of steps)."""
+    import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(i, budget_s) for i in range(procs)])
+    barrier, q = ctx.Barrier(procs), ctx.Queue()
+    ps = [ctx.Process(target=_pool_entry, args=(fn, i, budget_s, barrier, q), daemon=True) for i in range(procs)]
+    for p in ps:
+        p.start()
+    try:
+        res = [q.get(timeout=budget_s + 900)[1] for _ in ps]
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    bad = [r for r in res if not isinstance(r, tuple)]
+    if bad:
+        raise RuntimeError(f"CPU baseline worker failed: {bad[0]}")
     steps = sum(r[0] for r in res)
-    wall = max(r[1] for r in res)
-    return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x {budget_s:.1f} s of beergame-v0 episodes (construct + reset + 35 steps; "
-                      f"Poisson(8) demand, uniform [0,8] actions drawn before timing), one env per process, "
+    return steps / max(r[1] for r in res), steps
+
+
+def cpu_baseline(budget_s=2.5):
+    """Per-env NumPy restatement of BeerGameEnv.step on every host core (oracle, 'port')."""
+    cpus = host_cpus()
+    procs = cpus["procs"]
+    value, steps = cpu_pool(_cpu_worker, budget_s, procs)
+    return {"value": value, "unit": "env-steps/s", "cores": procs, "kind": "port", **cpus,
+            "budget_s": budget_s,
+            "sample": f"{procs} processes ({cpu_note(cpus)}) x {budget_s:.1f} s "
+                      f"of beergame-v0 episodes (construct + reset + 35 steps; Poisson(8) demand, uniform [0,8] "
+                      f"actions drawn before timing, timed parts started together), one env per process, "
                       f"oracle.beergame.BeerGameOracle (the reference step() statement for statement; "
                       f"profiles/r04_cpu_calibration.json); {steps} env-steps total"}
 
@@ -350,7 +427,7 @@ def parse_args(argv=None):
     ap.add_argument("--envs", type=int, default=N_ENVS, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the STREAM peak and beyond-cache point")
-    ap.add_argument("--cpu-budget", type=float, default=1.5)
+    ap.add_argument("--cpu-budget", type=float, default=2.5, help="seconds of CPU-baseline work per process")
     ap.add_argument("--kernel-samples", type=int, default=350,
                     help="launches timed one at a time with kernel-stamped events after the timed region")
     ap.add_argument("--no-dry-region", action="store_true",
@@ -408,7 +485,15 @@ class NodeBarrier:
         self._addr = ctypes.addressof(self._words)
 
     def __call__(self):
-        self._sense = self._fast(self._addr, self.world, self._sense, self._timeout_us)
+        if self._sense is None:
+            raise RuntimeError("the node barrier timed out earlier; its page is no longer usable")
+        try:
+            self._sense = self._fast(self._addr, self.world, self._sense, self._timeout_us)
+        except TimeoutError:
+            # this rank's arrival stays counted on the page and its sense did not advance, so
+            # every later barrier on it would release early or never: the page is dropped
+            self._sense = None
+            raise
 
 
 class Platform:
@@ -567,7 +652,8 @@ def run(args, plat):
     for e in ev + [x for pair in iso for x in pair]:
         plat.destroy_event(e)
     env.check_errors()
-    gather.result()
+    # the last episode end's all-gather against every rank's own returns (a collective)
+    gcheck = gather.verify()
     gather.close()
     elapsed, ep_elapsed, ep_gpu_ms, iso_ms, enq_s, drain_s, empty = max_over_ranks(
         [elapsed, ep_elapsed, ep_gpu_ms, iso_ms, split["enqueue_s"], split["drain_s"], empty], world, device, coll)
@@ -621,6 +707,11 @@ def run(args, plat):
                            "gpu_kernel_us_per_step": ep_gpu_ms * 1e3 / k_ep,
                            "bound": "host" if enq_s * 1e6 / args.steps > ep_gpu_ms * 1e3 / k_ep else "gpu"},
         "episode_returns_gathered": gather.gathers,
+        # the last gather: slice r == rank r's returns (EpisodeReturnGather.verify); main()
+        # exits non-zero when it does not hold
+        "allgather_ok": gcheck["allgather_ok"],
+        "gather_path": gcheck["gather_path"],
+        "allgather_envs_checked": gcheck["envs_checked"],
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = plat.cpu_baseline(args.cpu_budget)
@@ -636,6 +727,8 @@ def main(argv=None):
     if plat.collectives:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if line is not None and not line["allgather_ok"]:
+        sys.exit("bench: the episode-return all-gather does not hold every rank's returns in rank order")
 
 
 if __name__ == "__main__":

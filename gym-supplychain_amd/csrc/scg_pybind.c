@@ -117,7 +117,8 @@ static int64_t now_us(void) {
  * arrivals, words[1] is the phase. Every rank passes its last returned sense (0 at first);
  * the last to arrive resets the count and flips the phase, the others spin until it flips.
  * TimeoutError after timeout_us (a rank that never comes). The GIL is released while
- * waiting. */
+ * waiting. A timed-out call leaves its arrival counted and the caller's sense unchanged, so
+ * the page is unusable afterwards (bench.NodeBarrier drops it). */
 static PyObject* node_barrier(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
   (void)self;
   void* p;

@@ -634,6 +634,13 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
     for (int p = 0; p < P; ++p) {
       if (nd.n_init[p] < 0 || nd.n_init[p] > SCG_SC_MAX_INIT)
         return fail(SCG_ERR_INVALID, "node %d: %d initial pipeline entries (max %d)", i, nd.n_init[p], SCG_SC_MAX_INIT);
+      // the reference pushes its initial pipeline at times 1..k (SC_Node.reset :402-412);
+      // the ABI takes any time in [1, SCG_SC_MAX_INIT + lead time], which the heap-capacity
+      // simulation below indexes
+      for (int j = 0; j < nd.n_init[p]; ++j)
+        if (nd.init_time[p][j] < 1 || nd.init_time[p][j] > SCG_SC_MAX_INIT + std::max(cfg->avg_leadtime, cfg->max_leadtime))
+          return fail(SCG_ERR_INVALID, "node %d: initial pipeline time %d outside 1..%d", i, nd.init_time[p][j],
+                      SCG_SC_MAX_INIT + std::max(cfg->avg_leadtime, cfg->max_leadtime));
       if (nd.stock_capacity[p] <= 0) return fail(SCG_ERR_INVALID, "node %d: stock_capacity must be > 0", i);
       if (nd.processing_capacity > 0 && nd.processing_ratio[p] == 0)
         return fail(SCG_ERR_INVALID, "node %d: processing node with zero processing ratio", i);
@@ -713,10 +720,12 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
       want = SCG_SC_KERNEL_NODES;
   }
   // the staged kernel's byte-packed entries hold times up to kStagedMaxRel after the step's
-  // (scg_supplychain_staged.h): lead times, and the initial pipeline at times 1..k
+  // (scg_supplychain_staged.h): lead times, and the initial pipeline's times (1..k from the
+  // reference's reset, any validated time from a C-ABI caller)
   int rel_max = std::max(cfg->avg_leadtime, cfg->max_leadtime);
   for (int i = 0; i < NN; ++i)
-    for (int p = 0; p < P; ++p) rel_max = std::max(rel_max, nodes[i].n_init[p]);
+    for (int p = 0; p < P; ++p)
+      for (int j = 0; j < nodes[i].n_init[p]; ++j) rel_max = std::max(rel_max, nodes[i].init_time[p][j]);
   const bool staged_ok = rel_max <= kStagedMaxRel;
   if (want == SCG_SC_KERNEL_AUTO && staged_ok && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
     std::vector<scg_sc_node> probe(nodes, nodes + NN);

@@ -306,6 +306,55 @@ def hip_runtime():
     return _hip
 
 
+class MappedBuffer:
+    """Pinned host memory the GPU reads and writes directly (hipHostMalloc, mapped and
+    coherent): `host` / `dev` are its host and device addresses, `view(dtype, offset,
+    count)` a NumPy array over part of it. The single-env facades put their action,
+    observation and reward there, so a step is one launch and one stream synchronisation
+    with no copies (the kernel's loads and stores cross PCIe)."""
+
+    def __init__(self, nbytes):
+        hip = hip_runtime()
+        hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        hip.hipHostFree.argtypes = [ctypes.c_void_p]
+        hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+        self.nbytes = max(64, (int(nbytes) + 63) // 64 * 64)
+        host = ctypes.c_void_p()
+        # hipHostMallocMapped | hipHostMallocCoherent: the kernel's stores reach the host
+        # without depending on HIP_HOST_COHERENT
+        if hip.hipHostMalloc(ctypes.byref(host), self.nbytes, 0x2 | 0x40000000) != 0:
+            raise RuntimeError("hipHostMalloc failed")
+        dev = ctypes.c_void_p()
+        if hip.hipHostGetDevicePointer(ctypes.byref(dev), host, 0) != 0:
+            hip.hipHostFree(host)
+            raise RuntimeError("hipHostGetDevicePointer failed")
+        self._hip, self.host, self.dev = hip, host.value, dev.value
+        ctypes.memset(self.host, 0, self.nbytes)
+
+    def view(self, dtype, offset, count):
+        import numpy as np
+        dt = np.dtype(dtype)
+        if offset < 0 or offset % dt.itemsize or offset + count * dt.itemsize > self.nbytes:
+            raise ValueError("view outside the mapped buffer")
+        buf = (ctypes.c_char * (count * dt.itemsize)).from_address(self.host + offset)
+        return np.frombuffer(buf, dtype=dt, count=count)
+
+    def __del__(self):
+        try:
+            self._hip.hipHostFree(ctypes.c_void_p(self.host))
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass
+
+
+def stream_synchronize_fn():
+    """hipStreamSynchronize(raw stream) -> int, one ctypes call."""
+    hip = hip_runtime()
+    f = hip.hipStreamSynchronize
+    f.argtypes = [ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    return f
+
+
 class MappedWord:
     """One int32 of pinned host memory the GPU can write (hipHostMalloc, mapped): `dev` is
     its device address for kernels, `value` reads it on the host without synchronising."""
@@ -331,10 +380,6 @@ class MappedWord:
     @property
     def value(self):
         return self._word.value
-
-    @value.setter
-    def value(self, v):
-        self._word.value = int(v)
 
     @value.setter
     def value(self, v):

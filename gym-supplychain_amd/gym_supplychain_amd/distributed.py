@@ -190,9 +190,12 @@ class EpisodeReturnGather:
     tensor. With one process it degenerates to the snapshot, unless `collective` asks for
     the all-gather anyway (a one-rank rehearsal of the RCCL path; default: world > 1).
 
-    On GPUs with an nccl (RCCL) group the gather runs on a communicator of its own
-    (_RcclAllGather); SCG_GATHER=torch keeps it on dist.all_gather_into_tensor, which is also
-    the path of any other backend (gloo: the CPU tests).
+    The gather runs on dist.all_gather_into_tensor (RCCL on an nccl group, gloo on the
+    CPU). SCG_GATHER=rccl puts it on a communicator of the package's own instead
+    (_RcclAllGather: ≈10 µs less host time per episode end, profiles/r04p_gather_probe.log),
+    which has run at one rank only; it stays opt-in until a multi-GPU record shows it agreeing
+    with torch's. `path` names the one in use ("torch", "rccl-own", or "local" without a
+    collective) and verify() checks the latest gather's content.
     """
 
     def __init__(self, n_per_rank, device, group=None, collective=None):
@@ -203,20 +206,26 @@ class EpisodeReturnGather:
         self.collective = self.world > 1 if collective is None else bool(collective)
         if self.collective and not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("the return all-gather needs an initialised torch.distributed process group")
+        if self.collective:  # the rank of this process within the gather's group
+            self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self._stage = torch.zeros(self.n, dtype=torch.int64, device=self.device) if self.collective else None
         self._out = torch.zeros(self.world * self.n, dtype=torch.int64, device=self.device)
         self._work = None
         self._rccl = None
+        self._last = None  # the tensor handed to the latest on_episode_end
+        self.path = "torch" if self.collective else "local"
         if self.collective and self.device.type == "cuda" and dist.get_backend(group) == "nccl" \
-                and os.environ.get("SCG_GATHER", "rccl") != "torch":
+                and os.environ.get("SCG_GATHER", "torch") == "rccl":
             try:  # every rank takes the same branch (agree() inside)
                 self._rccl = _RcclAllGather(group, self.device)
+                self.path = "rccl-own"
             except RuntimeError as exc:
                 import warnings
                 warnings.warn(f"episode-return gather falls back to dist.all_gather_into_tensor: {exc}")
         self.gathers = 0
 
     def on_episode_end(self, final_return):
+        self._last = final_return
         if not self.collective:  # the snapshot is the result: one device copy per episode
             _async_copy(self._out, final_return)
             self.gathers += 1
@@ -241,6 +250,43 @@ class EpisodeReturnGather:
             self._work.wait()
             self._work = None
         return self._out
+
+    @staticmethod
+    def _checksums(x):
+        """(sum, sum of (j + 1) * x_j) of an int64 vector: position-sensitive, so a slice that
+        is shifted, reordered or another rank's shard does not match (int64 wraps alike)."""
+        w = torch.arange(1, x.numel() + 1, dtype=torch.int64, device=x.device)
+        return torch.stack([x.sum(), (x * w).sum()])
+
+    def verify(self):
+        """Check the latest gather (a collective when the gather is: every rank calls it).
+
+        * this rank's slice of the gathered tensor equals its local snapshot, and the snapshot
+          equals the tensor it was taken from (still holding the last episode's returns when
+          no episode ended since, as in bench.py after its last gather);
+        * slice r equals rank r's own snapshot, compared through per-rank checksums that
+          travel on dist.all_gather_into_tensor — an independent collective from the one
+          checked when the gather runs on the package's own communicator.
+        Returns {"allgather_ok": bool, "gather_path": str, "envs_checked": int}; the flag is
+        the same on every rank (agree)."""
+        out = self.result()
+        if self.gathers == 0:
+            return {"allgather_ok": True, "gather_path": self.path, "envs_checked": 0}
+        local = self._stage if self.collective else out
+        mine = out[self.rank * self.n:(self.rank + 1) * self.n]
+        ok = bool(torch.equal(mine, local))
+        if self._last is not None and self._last.numel() == self.n:
+            ok &= bool(torch.equal(local, self._last.to(local.device)))
+        if self.collective:
+            on = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+            cs = self._checksums(local).to(on)
+            every = torch.empty(self.world * 2, dtype=torch.int64, device=on)
+            dist.all_gather_into_tensor(every, cs, group=self.group)
+            want = every.view(self.world, 2).cpu()
+            got = torch.stack([self._checksums(out[r * self.n:(r + 1) * self.n]) for r in range(self.world)]).cpu()
+            ok &= bool(torch.equal(got, want))
+            ok = agree(ok, self.group, self.device)
+        return {"allgather_ok": ok, "gather_path": self.path, "envs_checked": self.world * self.n}
 
     def close(self):
         """Release the RCCL communicator (synchronises)."""

@@ -543,12 +543,14 @@ class BeerGameEnv(spaces.Env):
     def __init__(self, env_init_info={}, device=None):  # noqa: B006 - reference signature (:11)
         self.DEBUG = False
         cfg = BeerGameConfig(env_init_info)
-        # the reference's whole absolute-week shipment table (:46-50), for any horizon and delays
+        # the reference's whole absolute-week shipment table (:46-50), for any horizon and
+        # delays; separate state buffers (not the slab), so the overflow word can live in
+        # host-mapped memory below
         self._vec = BeerGameVecEnv(1, env_init_info, demand="fixed", device=device, auto_reset=False,
                                    track_costs=True, track_history=True, track_returns=False, config=cfg,
-                                   full_table=True)
+                                   full_table=True, state_slab=False)
         cfg = self._vec.config
-        self.levels = cfg.levels
+        self.levels = L = cfg.levels
         self.inv_cost = cfg.inv_cost
         self.backlog_cost = cfg.backlog_cost
         self.customer_demand = cfg.customer_demand.astype(np.int64)
@@ -558,14 +560,24 @@ class BeerGameEnv(spaces.Env):
         self.initial_shipment_value = cfg.initial_shipment_value
         self.initial_orders_value = cfg.initial_orders_value
         self.current_state = None
-        pin = torch.cuda.is_available()
-        self._act_host = torch.zeros((1, self.levels), dtype=torch.int32, pin_memory=pin)
-        self._act_np = self._act_host.numpy()
-        self._act_dev = torch.zeros((1, self.levels), dtype=torch.int32, device=self._vec.device)
-        self._out_host = torch.zeros(self._vec._out.shape, dtype=torch.int32, pin_memory=pin)
-        self._out_np = self._out_host.numpy()
-        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
-        self._err_np = self._err_host.numpy()
+        # one host-mapped block for the step's inputs and outputs: the overflow word (the
+        # kernel's plain store of 1, cleared by reset), the action row, and the observation
+        # row + reward; a step is one launch and one stream synchronisation, no copies
+        # (profiles/r05*_facade_latency.log)
+        ra = (4 * L + 15) // 16 * 16
+        self._io = io = nat.MappedBuffer(16 + ra + 4 * (L + 1))
+        self._err_np = io.view(np.int32, 0, 1)
+        self._act_np = io.view(np.int32, 16, L)
+        self._out_np = io.view(np.int32, 16 + ra, L + 1)
+        self._act_dev = io.dev + 16
+        vec = self._vec
+        vec._st.error_flags = io.dev
+        vec._err = torch.from_numpy(self._err_np)  # check_errors() reads the mapped word
+        self._step_args = nat.BgStepArgs(vec._cfg_addr, vec._st_addr, io.dev + 16 + ra, io.dev + 16 + ra + 4 * L,
+                                         vec._term_ptr, 0)
+        self._handle = ctypes.addressof(self._step_args)
+        self._fast_step_h = nat.fast.bg_step_h
+        self._sync = nat.stream_synchronize_fn()
         self._last_act = None
         self.week = None
 
@@ -582,17 +594,19 @@ class BeerGameEnv(spaces.Env):
         a = np.asarray(action)
         if a.dtype.kind == "f":
             a = np.trunc(a)
-        self._act_np[0, :] = np.broadcast_to(a, (self.levels,))
-        self._act_dev.copy_(self._act_host, non_blocking=True)
-        obs, _, done, _ = self._vec.step(self._act_dev)
-        self._out_host.copy_(self._vec._out, non_blocking=True)
-        self._err_host.copy_(self._vec._err, non_blocking=True)
-        torch.cuda.current_stream(self._vec.device).synchronize()
+        self._act_np[:] = np.broadcast_to(a, (self.levels,))
+        stream = self._vec._raw_stream(self._vec._dev_index)
+        r = self._fast_step_h(self._handle, self._act_dev, stream)
+        if r > 1:
+            nat.check(r >> 1)
+        rc = self._sync(stream)
+        if rc:
+            raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
         if int(self._err_np[0]):  # the reference's int64 values no longer fit the int32 state
             raise OverflowError("a BeerGame value left int32 range; the GPU state no longer matches the reference")
         L = self.levels
         self.week = self._vec.week
-        self._last_act = self._act_np[0].astype(np.int64)
+        self._last_act = self._act_np.astype(np.int64)
         self.current_state = self._out_np[:L].astype(np.int64)
         reward = np.int64(self._out_np[L])
         if self.DEBUG:

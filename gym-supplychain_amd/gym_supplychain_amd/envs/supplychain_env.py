@@ -493,8 +493,9 @@ class SupplyChainVecEnv:
             raise RuntimeError("in-transit heap capacity exceeded; results are invalid")
 
     # checkpoint / resume (gym_supplychain_amd/checkpoint.py) ------------------
-    # config fields that pick a kernel, not the chain: a checkpoint moves between kernels
-    _CKPT_SKIP = ("kernel", "layout", "group", "level_staged", "inbox_size")
+    # kernel-choice outputs of scg_sc_prepare: a checkpoint moves between kernels (the level
+    # kernel alone fills the level schedule)
+    _CKPT_SKIP = ("kernel", "layout", "group", "level_staged", "inbox_size", "n_levels", "level_start")
 
     def _ckpt_buffers(self):
         """Every device buffer that carries state from one step to the next, heaps and stocks
@@ -699,12 +700,16 @@ class SupplyChainEnv(spaces.Env):
         self.current_reward = 0
         self.customer_demands = None
         self.leadtimes = None
-        pin = torch.cuda.is_available()
-        self._act_host = torch.zeros((1, spec.n_actions), dtype=torch.float32, pin_memory=pin)
-        self._act_np = self._act_host.numpy()
-        self._act_dev = torch.zeros((1, spec.n_actions), dtype=torch.float32, device=self._vec.device)
-        self._obs_host = torch.zeros((1, spec.n_obs), dtype=torch.float64, pin_memory=pin)
-        self._rew_host = torch.zeros(1, dtype=torch.float64, pin_memory=pin)
+        # the step's action, observation and reward in one host-mapped block: a step is one
+        # launch and one stream synchronisation, no copies (profiles/r05*_facade_latency.log)
+        A, O = spec.n_actions, spec.n_obs
+        ra = (4 * A + 15) // 16 * 16
+        self._io = io = nat.MappedBuffer(ra + 8 * O + 8)
+        self._act_np = io.view(np.float32, 0, A).reshape(1, A)
+        self._obs_np = io.view(np.float64, ra, O)
+        self._rew_np = io.view(np.float64, ra + 8 * O, 1)
+        self._io_ptrs = (io.dev, io.dev + ra, io.dev + ra + 8 * O)
+        self._sync = nat.stream_synchronize_fn()
         self.build_info = spec.build_info
         self.est_episode = None
 
@@ -759,13 +764,17 @@ class SupplyChainEnv(spaces.Env):
         if a.size < n:  # the reference's per-node slices run past the end (:716-717 -> act)
             raise IndexError(f"action has {a.size} values, the chain needs {n}")
         self._act_np[0, :] = a[:n]  # like the reference, values beyond the chain's actions are unused
-        self._act_dev.copy_(self._act_host, non_blocking=True)
-        obs, rew, done, _ = self._vec.step(self._act_dev)
-        self._obs_host.copy_(obs, non_blocking=True)
-        self._rew_host.copy_(rew, non_blocking=True)
-        torch.cuda.current_stream(self._vec.device).synchronize()
-        self.current_state = self._obs_host.numpy()[0].copy()
-        self.current_reward = np.float64(self._rew_host.numpy()[0])
+        v = self._vec
+        stream = nat.raw_stream(v._dev_index)
+        act, obs, rew = self._io_ptrs
+        r = nat.fast.sc_step(v._cfg_addr, v._st_addr, act, obs, rew, v._term_ptr, v._flags, stream)
+        if r > 1:
+            nat.check(r >> 1)
+        rc = self._sync(stream)
+        if rc:
+            raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
+        self.current_state = self._obs_np.copy()
+        self.current_reward = np.float64(self._rew_np[0])
         self.episode_rewards += self.current_reward
         if self.time_step == self.total_time_steps:
             self._vec.check_errors()

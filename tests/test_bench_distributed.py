@@ -260,6 +260,51 @@ def test_bench_run_emits_the_rank0_line(world):
     # the walk to the boundary + 3,500 + 35 isolated steps
     total = 35 + 20 + 20 + (35 - (35 + 20 + 20) % 35) % 35 + 3500 + 35
     assert line["episode_returns_gathered"] == total // 35 == res[0]["ends"]
+    # the line's own content check of the last gather (EpisodeReturnGather.verify)
+    assert line["allgather_ok"] is True and line["gather_path"] == "torch"
+    assert line["allgather_envs_checked"] == world * n
+
+
+def _verify_worker(rank, world, port, q, corrupt):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gym_supplychain_amd.distributed import EpisodeReturnGather
+        g = EpisodeReturnGather(3, "cpu")
+        src = torch.tensor([100 * rank + 1, 100 * rank + 2, 100 * rank + 3], dtype=torch.int64)
+        g.on_episode_end(src)
+        out = g.result()
+        if corrupt == "swap" and rank == 1:      # two ranks' shards exchanged in this rank's copy
+            a = out[0:3].clone()
+            out[0:3] = out[3:6]
+            out[3:6] = a
+        elif corrupt == "stale" and rank == 0:   # the source changed after the snapshot
+            src += 1
+        elif corrupt == "value" and rank == 2:   # one element of another rank's slice off by one
+            out[1] += 1
+        q.put((rank, g.verify()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [None, "swap", "stale", "value"])
+def test_gather_verify_catches_a_wrong_gather(corrupt):
+    """EpisodeReturnGather.verify() on 3 gloo ranks: true for a correct gather; false on
+    every rank when one rank's gathered tensor has two shards swapped, one element of another
+    rank's slice differs, or the snapshot no longer matches its source."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_verify_worker, args=(r, 3, port, q, corrupt)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(3):
+        assert res[r]["allgather_ok"] is (corrupt is None)
+        assert res[r]["gather_path"] == "torch" and res[r]["envs_checked"] == 9
 
 
 def _barrier_worker(rank, world, port, q, arr, iters):
@@ -340,3 +385,16 @@ def test_node_barrier_setup_fails_on_every_rank_together():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert set(res.values()) == {"raised"}
+
+
+def test_node_barrier_is_dropped_after_a_timeout():
+    """A rank alone at the barrier times out; the page then refuses further use instead of
+    releasing a later barrier early (its arrival stays counted)."""
+    import bench
+    from gym_supplychain_amd.distributed import agree
+    bar = bench.NodeBarrier(0, 2, lambda ok: ok, timeout_s=0.05)
+    with pytest.raises(TimeoutError):
+        bar()
+    with pytest.raises(RuntimeError, match="no longer usable"):
+        bar()
+    assert agree is not None

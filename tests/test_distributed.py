@@ -98,8 +98,8 @@ def test_entropy_seed_group_needs_a_process_group():
     assert entropy_seed(7, seed_group=True) == 7
 
 
-def _rccl_gather_worker(port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+def _rccl_gather_worker(port, q, path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", SCG_GATHER=path)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
@@ -115,25 +115,32 @@ def _rccl_gather_worker(port, q):
                 got.append(g.result().clone())  # waited on the current stream, then read
         got.append(g.result().clone())
         want = [torch.arange(4096, device=dev) * (k + 1) - 7 for k in (1, 3, 4)]
-        q.put((g._rccl is not None, all(bool((a == b).all()) for a, b in zip(got, want)), g.gathers))
+        check = g.verify()
+        src.add_(1)  # the snapshot no longer matches its source: verify must say so
+        stale = g.verify()
+        q.put((g.path, all(bool((a == b).all()) for a, b in zip(got, want)), g.gathers, check, stale))
         g.close()
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-def test_rccl_return_gather_on_one_rank():
-    """EpisodeReturnGather on an nccl group runs on its own RCCL communicator (side stream,
-    event-ordered): every result() holds the snapshot of the latest episode end even though
-    the source buffer is rewritten right after."""
+@pytest.mark.parametrize("path", ["rccl", "torch"])
+def test_rccl_return_gather_on_one_rank(path):
+    """EpisodeReturnGather on an nccl group — torch's all_gather_into_tensor (the default) or,
+    with SCG_GATHER=rccl, the package's own communicator (side stream, event-ordered): every
+    result() holds the snapshot of the latest episode end even though the source buffer is
+    rewritten right after, and verify() checks the last gather (bench.py's allgather_ok)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    p = ctx.Process(target=_rccl_gather_worker, args=(port, q))
+    p = ctx.Process(target=_rccl_gather_worker, args=(port, q, path))
     p.start()
-    used_rccl, ok, n = q.get(timeout=240)
+    used, ok, n, check, stale = q.get(timeout=240)
     p.join(timeout=60)
     assert p.exitcode == 0
-    assert used_rccl and ok and n == 5
+    assert used == {"rccl": "rccl-own", "torch": "torch"}[path] and ok and n == 5
+    assert check == {"allgather_ok": True, "gather_path": used, "envs_checked": 4096}
+    assert stale["allgather_ok"] is False

@@ -259,3 +259,35 @@ def test_staged_kernel_takes_lead_times_its_bytes_hold(lt):
                 assert rc == nat.SCG_ERR_INVALID and "lead times" in nat.last_error()
         else:
             assert rc == 0 and (lt <= 30 or c.kernel != nat.SC_KERNEL_STAGED)
+
+
+@pytest.mark.parametrize("init_time", [30, 31, 0, 64])
+def test_initial_pipeline_times_bound_the_staged_kernel(init_time):
+    """A C-ABI caller's initial pipeline times (the reference's reset uses 1..k, :402-412):
+    the staged kernel's byte-packed entries hold times up to 30 after the step's, so a time
+    past that makes scg_sc_prepare refuse kernel='staged' and kernel='auto' pick another
+    kernel; a time outside 1..SCG_SC_MAX_INIT + lead time is refused by every kernel."""
+    import ctypes
+    from gym_supplychain_amd import _native as nat
+    from gym_supplychain_amd.envs import SupplyChainSpec
+    meta = load_sc("2perstage")["meta"]
+    kw = dict(meta["kwargs"], stochastic_leadtimes=False, avg_leadtime=20, max_leadtime=20)
+    spec = SupplyChainSpec(meta["nodes_info"], **kw)
+    for kernel in (nat.SC_KERNEL_STAGED, nat.SC_KERNEL_AUTO, nat.SC_KERNEL_LANE):
+        nodes = spec.node_table()
+        nodes[3].init_time[0][0] = init_time
+        c = nat.ScConfig()
+        c.n_nodes, c.n_products, c.n_retailers = len(spec.nodes), spec.P, spec.n_retailers
+        c.total_time_steps, c.avg_leadtime, c.max_leadtime = spec.total_time_steps, 20, 20
+        c.demand_lo, c.demand_hi = spec.demand_models[0].lo, spec.demand_models[0].hi
+        for k, v in spec.penalties.items():
+            setattr(c, k, v)
+        c.kernel = kernel
+        rc = nat.lib.scg_sc_prepare(ctypes.byref(c), nodes)
+        if not 1 <= init_time <= 16 + 20:
+            assert rc == nat.SCG_ERR_INVALID and "initial pipeline time" in nat.last_error()
+        elif kernel == nat.SC_KERNEL_STAGED and init_time > 30:
+            assert rc == nat.SCG_ERR_INVALID and "lead times" in nat.last_error()
+        else:
+            assert rc == 0, nat.last_error()
+            assert init_time <= 30 or c.kernel != nat.SC_KERNEL_STAGED

@@ -37,8 +37,7 @@ SCENARIOS = {
 }
 
 
-def _cpu_worker(arg):
-    name, idx, budget = arg
+def _cpu_worker(name, idx, budget, start):
     import numpy as np
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.environ.get("SCG_PKG_ROOT") or os.path.join(REPO, "gym-supplychain_amd"))
@@ -54,6 +53,7 @@ def _cpu_worker(arg):
     o = SupplyChainOracle(nodes, **okw)
     T, R, P = okw["total_time_steps"], len(o.retailers), o.P
     rng = np.random.RandomState(idx)
+    start()  # every worker's chain is built: the timed parts start together
     steps, ep = 0, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget:
@@ -67,18 +67,17 @@ def _cpu_worker(arg):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(name, budget=1.5, max_procs=16):
-    import multiprocessing as mp
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    procs = max(1, min(max_procs, cores))
-    with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(name, i, budget) for i in range(procs)])
-    steps = sum(r[0] for r in res)
-    return {"value": steps / max(r[1] for r in res), "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x {budget} s of {SCENARIOS[name]['env_id']} steps, one env per process, "
+def cpu_baseline(name, budget=2.5):
+    """SupplyChainOracle on every core of the affinity mask (bench.host_cpus / cpu_pool)."""
+    import functools
+
+    from bench import cpu_note, cpu_pool, host_cpus
+    cpus = host_cpus()
+    procs = cpus["procs"]
+    value, steps = cpu_pool(functools.partial(_cpu_worker, name), budget, procs)
+    return {"value": value, "unit": "env-steps/s", "cores": procs, "kind": "port", **cpus, "budget_s": budget,
+            "sample": f"{procs} processes ({cpu_note(cpus)}) x {budget} s of "
+                      f"{SCENARIOS[name]['env_id']} steps, one env per process, timed parts started together, "
                       f"oracle.supplychain.SupplyChainOracle; {steps} env-steps"}
 
 
