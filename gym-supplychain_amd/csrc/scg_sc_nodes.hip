@@ -27,7 +27,9 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "scg_common.h"
 #include "scg_supplychain_core.h"
@@ -97,223 +99,362 @@ struct TileWalk {
 #ifndef SCG_NODES_WPE
 #define SCG_NODES_WPE 4
 #endif
+// LDS-DMA (gfx950 global_load_lds_dwordx4): this lane's 16 bytes at `src` land at
+// lds_base + 16 * lane, lds_base wave-uniform; no VGPR holds the data, the wave's vmcnt
+// counts it.
+typedef __attribute__((address_space(3))) void* LdsPtr;
+typedef __attribute__((address_space(1))) void* GblPtr;
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((GblPtr)(const_cast<void*>(src)), (LdsPtr)(lds_base), 16, 0, 0);
+}
+
+// Rows [0, nrows) of a block's 64-env slab by LDS-DMA: global row r at src + r * gstride
+// bytes (the block's first env), LDS row r at dst + r * kRowBytes (256: int32 per env, 512:
+// double per env), 16 bytes per lane, 4 or 2 rows per wave instruction. Lanes whose bytes
+// lie past the block's `nb` envs read the row's first bytes instead (never used), so no lane
+// reads past the batch; nb is a multiple of 4 (scg_sc_step takes this path for N % 4 == 0).
+template <int kRowBytes>
+__device__ __forceinline__ void glds_rows(const char* src, int64_t gstride, char* dst, int nrows, int lane, int nb) {
+  constexpr int kLanesPerRow = kRowBytes / 16, kRowsPerInst = 64 / kLanesPerRow;
+  constexpr int kElem = kRowBytes / 64;  // bytes per env
+  const int col = (lane % kLanesPerRow) * 16;
+  const int c = col < nb * kElem ? col : 0;
+  for (int r0 = 0; r0 < nrows; r0 += kRowsPerInst) {  // wave-uniform
+    const int r = r0 + lane / kLanesPerRow;
+    if (r < nrows) glds16(src + r * gstride + c, dst + r0 * kRowBytes);
+  }
+}
+
+// Everything heap (i, p) and its stock need from HBM for a block's stage, by LDS-DMA in one
+// memory round: every heap slot (times and amounts), the size and the stock rows.
+__device__ __forceinline__ void nodes_dma_heap(const ScArgs& a, int hp, int H, int64_t n0, int nb, int lane,
+                                               int32_t* htk, double* hval, int32_t* hsz, double* stk) {
+  const int64_t N = a.n;
+  glds_rows<256>(reinterpret_cast<const char*>(a.tk + static_cast<int64_t>(hp) * H * N + n0), N * 4,
+                 reinterpret_cast<char*>(htk + hp * H * 64), H, lane, nb);
+  glds_rows<512>(reinterpret_cast<const char*>(a.val + static_cast<int64_t>(hp) * H * N + n0), N * 8,
+                 reinterpret_cast<char*>(hval + hp * H * 64), H, lane, nb);
+  glds_rows<256>(reinterpret_cast<const char*>(a.size + hp * N + n0), 0, reinterpret_cast<char*>(hsz + hp * 64), 1,
+                 lane, nb);
+  glds_rows<512>(reinterpret_cast<const char*>(a.stock + hp * N + n0), 0, reinterpret_cast<char*>(stk + hp * 64), 1,
+                 lane, nb);
+}
+
+// The block barrier while LDS-DMAs may be in flight: LDS writes made visible, memory
+// operations left outstanding (__syncthreads would wait for the DMAs too).
+__device__ __forceinline__ void barrier_lds_only() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+#ifndef SCG_NODES_PREFETCH
+#define SCG_NODES_PREFETCH 1
+#endif
+#ifndef SCG_NODES_LAUNDER
+#define SCG_NODES_LAUNDER 1
+#endif
+#ifndef SCG_NODES_DMA
+#define SCG_NODES_DMA 1
+#endif
+// The first tile of a block by LDS-DMA too (1) or by register loads (0: measured faster,
+// 37.6 against 40.4 us with no prefetch, profiles/r05c_nodes_persistent_ab.log); the
+// prefetched tiles always come by LDS-DMA.
+#ifndef SCG_NODES_DMA_FIRST
+#define SCG_NODES_DMA_FIRST 0
+#endif
+
 // Four waves per SIMD (<= 128 VGPRs): two blocks of eight waves per CU, which is also what
 // their LDS allows.
 // F64: float64 observations; LED: build_info ledgers (a separate instantiation, so the
 // ledger code costs the common run nothing).
+// Persistent: block b steps tiles b, b + gridDim.x, ... (64 envs each; the launch sizes the
+// grid to the blocks the device holds at once, so the second round of tiles needs no new
+// blocks). dma (N % 4 == 0): heaps, sizes and stocks arrive by LDS-DMA in one memory round,
+// and while a tile's last phases run, each wave's DMA brings the next tile's heaps, sizes and
+// stocks of its nodes into the LDS its nodes just released (the stocks into the other of two
+// stock buffers), so the next tile's stage waits only for its action rows.
 template <int MAXD, bool F64, bool LED>
 __global__ __launch_bounds__(64 * kNodesMaxWaves) __attribute__((amdgpu_waves_per_eu(SCG_NODES_WPE)))
-void sc_step_nodes_kernel(const ScArgs a, int W, int E) {
+void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
   using ObsT = typename std::conditional<F64, double, float>::type;
   extern __shared__ __align__(16) unsigned char smem[];
-  const ScCtx& c = a.c;
   // the wave index is wave-uniform: said so, node records are read with scalar loads
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * 64;
-  const int64_t n = n0 + lane;
-  const int nb = a.n - n0 < 64 ? static_cast<int>(a.n - n0) : 64;  // envs of this block
-  const bool live = lane < nb;
-  const int NN = c.n_nodes, P = c.P, NP = NN * P, H = c.H;
-  const int Ap = c.A | 1, Op = c.O | 1;  // odd row strides: lanes hit distinct banks
-  double* hval = reinterpret_cast<double*>(smem);
-  double* recv = hval + static_cast<int64_t>(NP) * H * 64;
-  double* ibval = recv + NP * 64;
-  double* cost_v = ibval + static_cast<int64_t>(E) * 64;
-  double* stk = cost_v + NN * 64;  // the block's stocks [NP][64] for the step
-  double* ret0 = stk + NP * 64;    // episode returns [64] (wave 0's prefetch)
-  ObsT* obs_t = reinterpret_cast<ObsT*>(ret0 + 64);
-  int32_t* htk = reinterpret_cast<int32_t*>(obs_t + 64 * Op);
-  int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
-  int32_t* ibtk = hsz + NP * 64;
-  int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
-  int32_t* amb = cost_k + NN * 64;
-  uint64_t* lword = reinterpret_cast<uint64_t*>(amb + W * 64);  // ledger entry marks and types [NP][64]
-  float* act_t = reinterpret_cast<float*>(lword + NP * 64);
-  // heaps and sizes in HBM (the batch's base pointers, column n); stocks in the LDS copy
-  ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
-  g.soff = lane;
-  g.hoff = n;
+  const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_tiles = (a_arg.n + 63) / 64;
   constexpr bool ledgers = LED;
-  if (ledgers) {  // the nodes' entries to their slots (column n = base + n0 + soff), reduced below
-    g.led_v = a.ledp_v + n0;
-    g.led_stride = a.n;
-    g.led_word = lword + lane;
-    g.led_word_stride = 64;
-  }
-  auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
-  NSTAMP(0);
+  // a tile's stocks and released sums take the two [NP][64] buffers in turn when the next
+  // tile's stocks were prefetched into the released-sum buffer
+  bool swapped = false, prefetched = false;
 
-  // the step's observation row, whichever buffer(s) it goes to (chosen at the copy-out)
-  ObsT* const orow = obs_t + lane * Op;
-  auto sink = [&](int o, double x) { orow[o] = static_cast<ObsT>(x); };
-  const NodesInbox in{ibtk + lane, ibval + lane, 64};
-  const float* act = act_t + lane * Ap;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    // the lane index, opaque to the compiler inside each tile: the per-lane LDS and HBM
+    // addresses derived from it are computed where used, not hoisted out of the tile loop
+    // and held in registers across it (which spilled the kernel at its 128-VGPR budget)
+#if SCG_NODES_LAUNDER
+    int lane;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
+#else
+    const int lane = lane0;
+#endif
+    // the launch arguments through a pointer the compiler cannot see across tiles: each tile
+    // reads them (scalar loads) and derives its addresses itself, instead of every derived
+    // value being hoisted out of the loop and held in scalar registers across it
+    typedef const __attribute__((address_space(4))) ScArgs* KArgPtr;
+    KArgPtr ap = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ap));
+    const ScArgs& a = *(const ScArgs*)ap;
+    const ScCtx& c = a.c;
+    const int NN = c.n_nodes, P = c.P, NP = NN * P, H = c.H;
+    const int Ap = c.A | 1, Op = c.O | 1;  // odd row strides: lanes hit distinct banks
+    double* hval = reinterpret_cast<double*>(smem);
+    double* sbuf0 = hval + static_cast<int64_t>(NP) * H * 64;  // two [NP][64] buffers: stocks / released sums
+    double* ibval = sbuf0 + NP * 64;
+    double* cost_v = ibval + static_cast<int64_t>(E) * 64;
+    double* sbuf1 = cost_v + NN * 64;
+    double* ret0 = sbuf1 + NP * 64;  // episode returns [64] (wave 0's prefetch)
+    ObsT* obs_t = reinterpret_cast<ObsT*>(ret0 + 64);
+    int32_t* htk = reinterpret_cast<int32_t*>(obs_t + 64 * Op);
+    int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
+    int32_t* ibtk = hsz + NP * 64;
+    int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
+    int32_t* amb = cost_k + NN * 64;
+    uint64_t* lword = reinterpret_cast<uint64_t*>(amb + W * 64);  // ledger entry marks and types [NP][64]
+    float* act_t = reinterpret_cast<float*>(lword + NP * 64);
+    double* const stk = swapped ? sbuf0 : sbuf1;
+    double* const recv = swapped ? sbuf1 : sbuf0;
+    const bool terminal = a.flags & 1;
+    const bool autoreset = a.flags & 2;
+    const int64_t n0 = tile * 64;
+    const int64_t n = n0 + lane;
+    const int nb = a.n - n0 < 64 ? static_cast<int>(a.n - n0) : 64;  // envs of this tile
+    const bool live = lane < nb;
+    auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
+    // heaps and sizes in HBM (the batch's base pointers, column n); stocks in the LDS copy
+    ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
+    g.soff = lane;
+    g.hoff = n;
+    if (ledgers) {  // the nodes' entries to their slots (column n = base + n0 + soff), reduced below
+      g.led_v = a.ledp_v + n0;
+      g.led_stride = a.n;
+      g.led_word = lword + lane;
+      g.led_word_stride = 64;
+    }
+#ifdef SCG_NODES_STAGGER_US
+    // experiment only: blocks [LO, HI) start late, so co-resident blocks run offset phases
+    if (tile == blockIdx.x && blockIdx.x >= SCG_NODES_STAGGER_LO && blockIdx.x < SCG_NODES_STAGGER_HI) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+      while (__builtin_amdgcn_s_memrealtime() - t0 < static_cast<uint64_t>(SCG_NODES_STAGGER_US * 100))
+        __builtin_amdgcn_s_sleep(8);
+    }
+#endif
+    NSTAMP(0);
 
-  // stage, one memory round: every thread requests its share of the block's action rows
-  // (one contiguous span), every wave its node's stocks, heap sizes and the first kStage
-  // slots of each heap, wave 0 the episode returns; nothing is waited for until all are in
-  // flight. Then everything to LDS, the rest of a longer heap, and what each heap releases.
-  bool bad = false;
-  {
-    constexpr int kAct = 4;  // action elements per thread per round
-    const float* src = a.act + n0 * c.A;
-    const int na = nb * c.A;
-    float av[kAct];
-#pragma unroll
-    for (int u = 0; u < kAct; ++u)
-      if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
-    const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
-    for (int i = w; i < NN; i += W)
-      for (int p = 0; p < P; ++p) {
-        const int hp = i * P + p;
-        if (!live) continue;
-        const int64_t r = static_cast<int64_t>(hp) * a.n + n;
-        const double st = a.stock[r];
-        const int32_t sz = a.size[r];
-        stk[hp * 64 + lane] = st;
-        hsz[hp * 64 + lane] = sz;
-        const HeapView lh = lheap(hp);
-        // the heap's first slots are requested with the size (sc_nodes_copy_heap, shared
-        // with the host harness); a longer heap costs a round more
-        sc_nodes_copy_heap(HeapView{a.tk + static_cast<int64_t>(hp) * H * a.n + n,
-                                    a.val + static_cast<int64_t>(hp) * H * a.n + n, a.n},
-                           lh, H, sz);
-        bad |= !sc_recv_scan(lh, sz, a.t, recv[hp * 64 + lane]);
-      }
+    // the step's observation row, whichever buffer(s) it goes to (chosen at the copy-out)
+    ObsT* const orow = obs_t + lane * Op;
+    auto sink = [&](int o, double x) { orow[o] = static_cast<ObsT>(x); };
+    const NodesInbox in{ibtk + lane, ibval + lane, 64};
+    const float* act = act_t + lane * Ap;
+
+    // stage, one memory round: every thread requests its share of the tile's action rows
+    // (one contiguous span), wave 0 the episode returns, every wave its nodes' heaps, sizes
+    // and stocks (LDS-DMA, unless the previous tile prefetched them; else register loads and
+    // a round more for a longer heap); nothing is waited for until all are in flight. Then
+    // the actions to their LDS tile and what each heap releases.
+    bool bad = false;
     {
-      TileWalk tw(threadIdx.x, blockDim.x, c.A);
+      constexpr int kAct = 4;  // action elements per thread per round
+      const float* src = a.act + n0 * c.A;
+      const int na = nb * c.A;
+      float av[kAct];
 #pragma unroll
-      for (int u = 0; u < kAct; ++u, tw.next())
-        if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) act_t[tw.r * Ap + tw.k] = av[u];
-      for (int q = threadIdx.x + kAct * blockDim.x; q < na; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
-    }
-    if (w == 0 && live && a.ep_ret) ret0[lane] = r0;
-  }
-  amb[w * 64 + lane] = bad ? 1 : 0;
-  NSTAMP(5);
-  __syncthreads();
-  NSTAMP(6);
-  bool flagged = (a.flags & 4) != 0;
-  for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
-  const bool go = live && !flagged;
-
-  // act: every node at once (a node's act needs only what its own heaps release)
-  if (go)
-    for (int i = w; i < NN; i += W) {
-      const Num cst = sc_nodes_act<MAXD, !LED>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
-      cost_v[i * 64 + lane] = cst.v;
-      cost_k[i * 64 + lane] = cst.k;
-      for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
-    }
-  NSTAMP(1);
-  __syncthreads();
-  NSTAMP(2);
-
-  // heaps
-  if (go)
-    for (int i = w; i < NN; i += W) {
-      WordCache ltc{0, U4{0, 0, 0, 0}, false};
-      int a_i = 0, lt_i = 0;
-      for (int p = 0; p < P; ++p) {
-        const int hp = i * P + p;
-        sc_nodes_heap(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, a.t, i, p, a_i, lt_i, sink);
+      for (int u = 0; u < kAct; ++u)
+        if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
+      const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
+      if (prefetched || (dma && SCG_NODES_DMA_FIRST)) {
+        if (!prefetched)
+          for (int i = w; i < NN; i += W)
+            for (int p = 0; p < P; ++p) nodes_dma_heap(a, i * P + p, H, n0, nb, lane, htk, hval, hsz, stk);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs (this tile's or the prefetch) have landed
+        for (int i = w; i < NN; i += W)
+          for (int p = 0; p < P; ++p) {
+            const int hp = i * P + p;
+            if (live) bad |= !sc_recv_scan(lheap(hp), hsz[hp * 64 + lane], a.t, recv[hp * 64 + lane]);
+          }
+      } else {
+        for (int i = w; i < NN; i += W)
+          for (int p = 0; p < P; ++p) {
+            const int hp = i * P + p;
+            if (!live) continue;
+            const int64_t r = static_cast<int64_t>(hp) * a.n + n;
+            const double st = a.stock[r];
+            const int32_t sz = a.size[r];
+            stk[hp * 64 + lane] = st;
+            hsz[hp * 64 + lane] = sz;
+            const HeapView lh = lheap(hp);
+            // the heap's first slots are requested with the size (sc_nodes_copy_heap, shared
+            // with the host harness); a longer heap costs a round more
+            sc_nodes_copy_heap(HeapView{a.tk + static_cast<int64_t>(hp) * H * a.n + n,
+                                        a.val + static_cast<int64_t>(hp) * H * a.n + n, a.n},
+                               lh, H, sz);
+            bad |= !sc_recv_scan(lh, sz, a.t, recv[hp * 64 + lane]);
+          }
       }
-    }
-  NSTAMP(3);
-
-  // ledgers: entry q of an env, the nodes' entries added in node order (:750-760); at an
-  // auto-reset the finished episode's ledger is kept and the new one starts at int 0
-  const bool terminal = a.flags & 1;
-  const bool autoreset = a.flags & 2;
-  auto ledger_put = [&](int q, double lv, int32_t lk) {
-    const int64_t at = q * a.n + n;
-    if (autoreset) {
-      if (a.led_fv) {
-        a.led_fv[at] = lv;
-        a.led_fk[at] = lk;
+      {
+        TileWalk tw(threadIdx.x, blockDim.x, c.A);
+#pragma unroll
+        for (int u = 0; u < kAct; ++u, tw.next())
+          if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) act_t[tw.r * Ap + tw.k] = av[u];
+        for (int q = threadIdx.x + kAct * blockDim.x; q < na; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
       }
-      lv = 0.0;
-      lk = np_kind_abi(NK_INT);
+      if (w == 0 && live && a.ep_ret) ret0[lane] = r0;
     }
-    a.led_v[at] = lv;
-    a.led_k[at] = lk;
-  };
-  // entries first, first + step, ... of an env, two at a time (their loads in flight together)
-  auto ledger_entries = [&](int first, int step) {
-    const int nq = 2 * SCG_SC_LEDGER_KEYS * P;
-    for (int q0 = first; q0 < nq; q0 += 2 * step) {
-      const int q1 = q0 + step < nq ? q0 + step : -1;
-      const int64_t at0 = q0 * a.n + n, at1 = (q1 >= 0 ? q1 : q0) * a.n + n;
-      double lv0 = a.led_v[at0], lv1 = a.led_v[at1];
-      int32_t lk0 = a.led_k[at0], lk1 = a.led_k[at1];
-      sc_ledger_reduce_pair(c, q0, q1, a.ledp_v + n, a.n, lword + lane, 64, lv0, lk0, lv1, lk1);
-      ledger_put(q0, lv0, lk0);
-      if (q1 >= 0) ledger_put(q1, lv1, lk1);
+    amb[w * 64 + lane] = bad ? 1 : 0;
+    NSTAMP(5);
+    __syncthreads();
+    NSTAMP(6);
+    bool flagged = (a.flags & 4) != 0;
+    for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
+    const bool go = live && !flagged;
+    // the next tile's heaps, sizes and stocks come by LDS-DMA as this tile's heaps finish
+    // (every wave reads the same flags: the decision is block-uniform). Not when an env of
+    // this tile steps serially (wave 0 reads every node's staged heaps after the heaps
+    // phase) or resets (the reset writes this tile's heaps).
+    const bool pf = SCG_NODES_PREFETCH && dma && tile + gridDim.x < n_tiles && !autoreset &&
+                    __builtin_amdgcn_ballot_w64(flagged) == 0;
+    const int64_t nn0 = (tile + gridDim.x) * 64;
+    const int nnb = pf ? (a.n - nn0 < 64 ? static_cast<int>(a.n - nn0) : 64) : 0;
+
+    // act: every node at once (a node's act needs only what its own heaps release)
+    if (go)
+      for (int i = w; i < NN; i += W) {
+        const Num cst = sc_nodes_act<MAXD, !LED>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
+        cost_v[i * 64 + lane] = cst.v;
+        cost_k[i * 64 + lane] = cst.k;
+        for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
+      }
+    NSTAMP(1);
+    __syncthreads();
+    NSTAMP(2);
+
+    // heaps; then the next tile's DMA into what this wave's nodes released (the released
+    // sums are dead since the act: the next stocks go there)
+    if (go)
+      for (int i = w; i < NN; i += W) {
+        WordCache ltc{0, U4{0, 0, 0, 0}, false};
+        int a_i = 0, lt_i = 0;
+        for (int p = 0; p < P; ++p) {
+          const int hp = i * P + p;
+          sc_nodes_heap(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, a.t, i, p, a_i, lt_i, sink);
+        }
+      }
+    if (pf) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of its heaps are done
+      for (int i = w; i < NN; i += W)
+        for (int p = 0; p < P; ++p) nodes_dma_heap(a, i * P + p, H, nn0, nnb, lane, htk, hval, hsz, recv);
     }
-  };
+    NSTAMP(3);
+
+    // ledgers: entry q of an env, the nodes' entries added in node order (:750-760); at an
+    // auto-reset the finished episode's ledger is kept and the new one starts at int 0
+    auto ledger_put = [&](int q, double lv, int32_t lk) {
+      const int64_t at = q * a.n + n;
+      if (autoreset) {
+        if (a.led_fv) {
+          a.led_fv[at] = lv;
+          a.led_fk[at] = lk;
+        }
+        lv = 0.0;
+        lk = np_kind_abi(NK_INT);
+      }
+      a.led_v[at] = lv;
+      a.led_k[at] = lk;
+    };
+    // entries first, first + step, ... of an env, two at a time (their loads in flight together)
+    auto ledger_entries = [&](int first, int step) {
+      const int nq = 2 * SCG_SC_LEDGER_KEYS * P;
+      for (int q0 = first; q0 < nq; q0 += 2 * step) {
+        const int q1 = q0 + step < nq ? q0 + step : -1;
+        const int64_t at0 = q0 * a.n + n, at1 = (q1 >= 0 ? q1 : q0) * a.n + n;
+        double lv0 = a.led_v[at0], lv1 = a.led_v[at1];
+        int32_t lk0 = a.led_k[at0], lk1 = a.led_k[at1];
+        sc_ledger_reduce_pair(c, q0, q1, a.ledp_v + n, a.n, lword + lane, 64, lv0, lk0, lv1, lk1);
+        ledger_put(q0, lv0, lk0);
+        if (q1 >= 0) ledger_put(q1, lv1, lk1);
+      }
+    };
 #if SCG_NODES_LED_EARLY
-  // Every slot and mark of an acted env is in place since the act barrier, so each wave
-  // reduces its share of the entries as soon as its heaps are done: the slot loads overlap
-  // the other waves' heaps and wave 0's reward instead of forming a phase of their own after
-  // the last barrier. A flagged env's slots are written by wave 0's serial walk below, which
-  // then reduces that env's entries itself.
-  if (ledgers && live && !flagged) ledger_entries(w, W);
+    // Every slot and mark of an acted env is in place since the act barrier, so each wave
+    // reduces its share of the entries as soon as its heaps are done: the slot loads overlap
+    // the other waves' heaps and wave 0's reward instead of forming a phase of their own after
+    // the last barrier. A flagged env's slots are written by wave 0's serial walk below, which
+    // then reduces that env's entries itself.
+    if (ledgers && live && !flagged) ledger_entries(w, W);
 #endif
 
-  // reward
-  if (w == 0 && live) {
-    double reward;
-    if (flagged) {  // untouched by act and heaps: the serial walk on its staged heaps
-      reward = sc_nodes_serial<MAXD, !LED>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
+    // reward
+    if (w == 0 && live) {
+      double reward;
+      if (flagged) {  // untouched by act and heaps: the serial walk on its staged heaps
+        reward = sc_nodes_serial<MAXD, !LED>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
 #if SCG_NODES_LED_EARLY
-      if (ledgers) ledger_entries(0, 1);
+        if (ledgers) ledger_entries(0, 1);
 #endif
-    } else {
-      Num total = pyint(0);
-      for (int i = 0; i < NN; ++i) total = np_add(total, Num{cost_v[i * 64 + lane], cost_k[i * 64 + lane]});
-      reward = np_neg(total).v;
+      } else {
+        Num total = pyint(0);
+        for (int i = 0; i < NN; ++i) total = np_add(total, Num{cost_v[i * 64 + lane], cost_k[i * 64 + lane]});
+        reward = np_neg(total).v;
+      }
+      a.rew[n] = reward;
+      if (a.ep_ret) {
+        const double r = ret0[lane] + reward;  // episode_rewards += current_reward (:739)
+        if (terminal && a.final_ret) a.final_ret[n] = r;
+        a.ep_ret[n] = autoreset ? 0.0 : r;
+      }
+      for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, a.t, k, sink);  // (:771)
+      sc_observe_tail(c, a.t, sink);                                               // (:786)
     }
-    a.rew[n] = reward;
-    if (a.ep_ret) {
-      const double r = ret0[lane] + reward;  // episode_rewards += current_reward (:739)
-      if (terminal && a.final_ret) a.final_ret[n] = r;
-      a.ep_ret[n] = autoreset ? 0.0 : r;
-    }
-    for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, a.t, k, sink);  // (:771)
-    sc_observe_tail(c, a.t, sink);                                               // (:786)
-  }
-  __syncthreads();
-  NSTAMP(7);
+    // an auto-reset below writes this tile's heaps in HBM after every wave's copy-back
+    // (__syncthreads waits for the stores); else the prefetch may stay in flight
+    if (autoreset)
+      __syncthreads();
+    else
+      barrier_lds_only();
+    NSTAMP(7);
 
 #if !SCG_NODES_LED_EARLY
-  if (ledgers && live) ledger_entries(w, W);
+    if (ledgers && live) ledger_entries(w, W);
 #endif
 
-  // out: the tile is this step's observation — obs, or the terminal observation when the
-  // env resets now (then wave 0 writes the reset observation to obs), or both
-  ObsT* const dst0 = static_cast<ObsT*>(autoreset ? a.term_obs : a.obs);
-  ObsT* const dst1 = (terminal && !autoreset) ? static_cast<ObsT*>(a.term_obs) : nullptr;
-  TileWalk tw(threadIdx.x, blockDim.x, c.O);
-  for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
-    const ObsT x = obs_t[tw.r * Op + tw.k];
-    if (dst0) dst0[n0 * c.O + q] = x;
-    if (dst1) dst1[n0 * c.O + q] = x;
-  }
-  if (autoreset) {  // after the barrier every wave's heap copy-back has landed
-    if (w == 0 && live) {
-      g.episode = a.episode + 1;
-      g.led_v = nullptr;   // the ledger was restarted above
-      sc_reset_env(c, g);  // heaps in HBM, stocks in the LDS copy
-      ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
-      sc_observe(c, g, 0, out);
+    // out: the tile is this step's observation — obs, or the terminal observation when the
+    // env resets now (then wave 0 writes the reset observation to obs), or both
+    ObsT* const dst0 = static_cast<ObsT*>(autoreset ? a.term_obs : a.obs);
+    ObsT* const dst1 = (terminal && !autoreset) ? static_cast<ObsT*>(a.term_obs) : nullptr;
+    TileWalk tw(threadIdx.x, blockDim.x, c.O);
+    for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
+      const ObsT x = obs_t[tw.r * Op + tw.k];
+      if (dst0) dst0[n0 * c.O + q] = x;
+      if (dst1) dst1[n0 * c.O + q] = x;
     }
-    __syncthreads();
+    if (autoreset) {  // after the barrier every wave's heap copy-back has landed
+      if (w == 0 && live) {
+        g.episode = a.episode + 1;
+        g.led_v = nullptr;   // the ledger was restarted above
+        sc_reset_env(c, g);  // heaps in HBM, stocks in the LDS copy
+        ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
+        sc_observe(c, g, 0, out);
+      }
+      __syncthreads();
+    }
+    if (live) {  // the stocks of this wave's nodes back, one 64-env row per instruction (the
+                 // next tile's stage rewrites these rows of the buffers: the same wave)
+      for (int i = w; i < NN; i += W)
+        for (int p = 0; p < P; ++p) a.stock[(i * P + p) * a.n + n] = stk[(i * P + p) * 64 + lane];
+      if (g.overflow) atomicOr(a.err, 1);
+    }
+    NSTAMP(4);
+    // the next tile: its stocks in the released-sum buffer when prefetched; the buffers the
+    // out phase still reads (the observation tile, this tile's stocks) are next written after
+    // the next tile's first barrier
+    swapped ^= pf;
+    prefetched = pf;
   }
-  if (live) {  // the stocks back, one 64-env row per instruction
-    for (int hp = w; hp < NP; hp += W) a.stock[hp * a.n + n] = stk[hp * 64 + lane];
-    if (g.overflow) atomicOr(a.err, 1);
-  }
-  NSTAMP(4);
 }
 
 // LDS bytes of one block (the layout above); obs_bytes 4 (float) or 8 (double).
@@ -346,6 +487,35 @@ size_t sc_nodes_lds_max() {
   return v;
 }
 
+// Blocks the device holds at once for this instantiation (occupancy x CUs), asked once per
+// device and shape; the persistent grid is that many blocks, or one per tile when fewer.
+template <int MAXD, bool F64, bool LED>
+int64_t sc_nodes_resident_blocks(int dev, int W, size_t lds) {
+  struct Entry {
+    int dev, W;
+    size_t lds;
+    int64_t blocks;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Entry& e : cache)
+    if (e.dev == dev && e.W == W && e.lds == lds) return e.blocks;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&sc_step_nodes_kernel<MAXD, F64, LED>),
+                                                   64 * W, lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
+    return 0;  // unknown: one block per tile
+  cache.push_back(Entry{dev, W, lds, static_cast<int64_t>(per_cu) * cus});
+  return cache.back().blocks;
+}
+
+#ifndef SCG_NODES_PERSISTENT
+#define SCG_NODES_PERSISTENT 1
+#endif
+
+std::atomic<int> g_nodes_max_blocks{0};  // scg_sc_nodes_max_blocks (tests)
+
 template <int MAXD, bool F64, bool LED>
 int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
   static std::atomic<bool> raised[64] = {};  // per device
@@ -359,8 +529,18 @@ int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
       return fail(SCG_ERR_HIP, "node-parallel kernel: cannot raise its LDS limit");
     raised[dev].store(true, std::memory_order_release);
   }
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_nodes_kernel<MAXD, F64, LED>), dim3(static_cast<unsigned>((a.n + 63) / 64)),
-                     dim3(64 * W), lds, s, a, W, E);
+  const int64_t tiles = (a.n + 63) / 64;
+  int64_t blocks = tiles;
+  if (SCG_NODES_PERSISTENT) {
+    const int64_t resident = sc_nodes_resident_blocks<MAXD, F64, LED>(dev, W, lds);
+    if (resident > 0 && resident < tiles) blocks = resident;
+  }
+  const int cap = g_nodes_max_blocks.load(std::memory_order_relaxed);
+  if (cap > 0 && cap < blocks) blocks = cap;
+  // the LDS-DMA stage reads whole 16-byte groups of a 64-env row: the batch a multiple of 4
+  const int dma = SCG_NODES_DMA && a.n % 4 == 0 ? 1 : 0;
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_nodes_kernel<MAXD, F64, LED>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(64 * W), lds, s, a, W, E, dma);
   return check_launch("sc_step_nodes_kernel");
 }
 
@@ -384,6 +564,10 @@ int sc_launch_nodes(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t 
 }
 
 }  // namespace scg
+
+extern "C" __attribute__((visibility("default"))) int scg_sc_nodes_max_blocks(int32_t blocks) {
+  return scg::g_nodes_max_blocks.exchange(blocks < 0 ? 0 : blocks);
+}
 
 #ifdef SCG_NODES_STAMPS
 // Diagnostic build only: copy the stamps of the first `waves` waves to host memory.

@@ -209,6 +209,9 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
 #endif
 // LED: build_info ledgers kept (a separate instantiation: without it every ledger note,
 // and the per-destination unit sums only ledgers read, compile away).
+#ifndef SCG_STAGED_KARG_CTX
+#define SCG_STAGED_KARG_CTX 1
+#endif
 template <int MAXD, bool LED>
 __global__ __launch_bounds__(kScBlock)
 #if SCG_STAGED_WPE
@@ -241,7 +244,11 @@ void sc_step_staged_kernel(const ScArgs a) {
     if (node_obs) main(o, x);
     if (both) extra(o, x);
   };
+#if SCG_STAGED_KARG_CTX
+  const double reward = sc_staged_step_ctx<MAXD, !LED>(KernargCtx{}, g, lh, in, a.act + n * c.A, a.t, sink);
+#else
   const double reward = sc_staged_step<MAXD, !LED>(c, g, lh, in, a.act + n * c.A, a.t, sink);
+#endif
   a.rew[n] = reward;
   if (a.ep_ret) {
     const double r = a.ep_ret[n] + reward;

@@ -39,6 +39,21 @@ struct ScArgs {
   int32_t layout;  // SCG_SC_LAYOUT_*
 };
 
+// The launch's ScCtx (the first member of ScArgs, the kernel's first argument) re-read
+// through the kernel-argument pointer laundered by an empty asm: the compiler cannot prove two
+// calls return the same object, so a loop over nodes loads context fields (scalar loads,
+// cached) where each iteration uses them instead of hoisting them and everything derived from
+// them out of the loop and holding them in scalar registers across it, which spilled them
+// into VGPR lanes. Only for kernels whose first argument is `const ScArgs`.
+struct KernargCtx {
+  __device__ __forceinline__ const ScCtx& operator()() const {
+    typedef const __attribute__((address_space(4))) ScArgs* KArgPtr;
+    KArgPtr ap = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ap));
+    return ((const ScArgs*)ap)->c;
+  }
+};
+
 struct ObsRow {
   void* base;
   int64_t row;

@@ -60,6 +60,39 @@ struct ScCtx {
   ConstTab<double> dbase;
 };
 
+// A wave-uniform pointer the compiler cannot follow across the call (device, kOpaque): loads
+// through it are issued where they are used, not hoisted to a loop's or an unrolled
+// sequence's top with their values held in scalar registers throughout, where a node's many
+// per-destination fields spilled into VGPR lanes. Identity otherwise.
+#ifndef SCG_SC_OPAQUE_DEST
+#define SCG_SC_OPAQUE_DEST 0
+#endif
+template <bool kOpaque, class T>
+__host__ __device__ __forceinline__ T* sc_opaque(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (kOpaque) asm volatile("" : "+s"(p));
+#endif
+  return p;
+}
+
+// A wave-uniform integer the compiler cannot follow (device): its multiples and the addresses
+// derived from it are computed where used rather than hoisted out of a loop and held — or
+// spilled — across it. Identity on the host.
+template <class T>
+__host__ __device__ __forceinline__ T sc_opaque_val(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(v));
+#endif
+  return v;
+}
+
+// The context of a loop over nodes as a callable (sc_staged_step_ctx): the caller's own. The
+// kernels pass KernargCtx (scg_supplychain_args.h) instead.
+struct HostCtx {
+  const ScCtx& c;
+  __host__ __device__ __forceinline__ const ScCtx& operator()() const { return c; }
+};
+
 // The demand models of a config: per product, or every product uniform on
 // [demand_lo, demand_hi] when the config gives none (host side of the launch).
 inline void sc_ctx_demand(ScCtx& c, const scg_sc_config* cfg) {
@@ -317,6 +350,7 @@ __host__ __device__ __forceinline__ void sc_push(const ScCtx& c, ScEnv& e, int n
 // destination does; a heap push keeps the loop rolled to bound code size).
 struct DirectPush {
   static constexpr bool kUnroll = false;
+  static constexpr bool kUniformNode = false;
   static constexpr bool kLdsSplit = false;  // see sc_split_scratch
   static constexpr bool kVecActions = false;  // see sc_ship_vals
   static constexpr bool kClearInAct = false;  // see StagedInbox::noship
@@ -643,6 +677,9 @@ __host__ __device__ __forceinline__ Num sc_node_act(const ScCtx& c, ScEnv& e, Wo
           // per-destination array besides the split's output stays live.
           Num leaving = pyint(0), ship_cost = pyint(0), ship_units = pyint(0);
           auto dest_step = [&](int i) {
+            // this destination's node fields, loaded here (Push::kUniformNode: the node is
+            // wave-uniform, so the laundered pointer stays in scalar registers)
+            ScNode& nd = *sc_opaque<Push::kUniformNode && SCG_SC_OPAQUE_DEST>(&c.nodes[ni]);
             Num o;
             if constexpr (Push::kLdsSplit)
               o = cut ? push.scratch_get(rank[i]) : pyint(0);

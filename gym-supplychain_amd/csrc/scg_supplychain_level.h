@@ -41,6 +41,7 @@ struct LevelInbox {
   int32_t src0, dst0, wsrc, wdst;
 
   static constexpr bool kUnroll = true;  // an LDS store per destination
+  static constexpr bool kUniformNode = false;  // the group's lanes act different nodes
   static constexpr bool kLdsSplit = false;
   static constexpr bool kVecActions = false;
   static constexpr bool kClearInAct = false;  // cleared before the act

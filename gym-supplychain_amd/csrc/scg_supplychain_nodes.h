@@ -41,6 +41,7 @@ struct NodesInbox {
   int64_t stride;
 
   static constexpr bool kUnroll = true;
+  static constexpr bool kUniformNode = true;  // a wave per node
   static constexpr bool kLdsSplit = false;
   static constexpr bool kVecActions = false;  // actions come from an LDS tile
   static constexpr bool kClearInAct = false;  // cleared before the act

@@ -59,6 +59,9 @@ struct HeapView8 {
 };
 
 // Shipments into the destinations' inbox entries; entry q of this env at [q * stride].
+#ifndef SCG_STAGED_OPAQUE_STRIDE
+#define SCG_STAGED_OPAQUE_STRIDE 0
+#endif
 struct StagedInbox {
   uint8_t* tk;  // (time - t) << 3 | kind, kStagedNone = no shipment
   double* val;
@@ -67,6 +70,7 @@ struct StagedInbox {
   int32_t t;      // the step's time: shipments are stored relative to it
 
   static constexpr bool kUnroll = true;  // a store per destination
+  static constexpr bool kUniformNode = true;  // one lane per env, nodes in turn: the node is wave-uniform
   static constexpr bool kLdsSplit = true;
   static constexpr bool kVecActions = true;  // the env's action row in HBM
 #ifndef SCG_STAGED_NOSHIP
@@ -93,7 +97,7 @@ struct StagedInbox {
   }
   __host__ __device__ __forceinline__ void ship(const ScCtx& c, ScEnv&, int src, int d, int /*dest*/, int p,
                                                 int32_t time, Num amount) const {
-    ScNode& nd = c.nodes[src];
+    ScNode& nd = *sc_opaque<SCG_SC_OPAQUE_DEST != 0>(&c.nodes[src]);
     const int64_t q = nd.in_slot[d] + static_cast<int64_t>(p) * nd.in_stride[d];
     tk[q * stride] = static_cast<uint8_t>(he_pack(time - t, amount.k));
     val[q * stride] = amount.v;
@@ -225,28 +229,47 @@ __host__ __device__ inline void sc_staged_heap(const ScCtx& c, ScEnv& g, const H
 // shares. out(o, x) receives the node observation elements (the caller adds the demand and
 // time-to-go ones). Returns the reward. (Staging the node's stocks in LDS as well measured
 // no faster on MI355X: stock accesses are few and cache-resident.)
-template <int MAXD, bool kKindPaths = false, class Sink>
-__host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView8& lh, const StagedInbox& in,
-                                                 const float* act, int t, Sink& out) {
+// ctx() gives the launch-uniform context; each node's iteration asks for it again (the
+// kernel's KernargCtx re-reads it through a pointer the compiler cannot see across
+// iterations, so nothing derived from it is held in registers across the node loop).
+template <int MAXD, bool kKindPaths = false, class CtxFn, class Sink>
+__host__ __device__ inline double sc_staged_step_ctx(const CtxFn& ctx, ScEnv& g, const HeapView8& lh,
+                                                     const StagedInbox& in, const float* act, int t, Sink& out) {
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   Num total = pyint(0);
   SCG_ACC_DECL
 #ifdef SCG_SC_STAMPS
   g.dbg = &scg_acc_;
 #endif
-  for (int i = 0; i < c.n_nodes; ++i) {
+  const int NN = ctx().n_nodes;
+  for (int i = 0; i < NN; ++i) {
+    const ScCtx& c = ctx();
     ScNode& nd = c.nodes[i];
+    // the batch strides (uniform: the env-fastest layout) made opaque per node, so their many
+    // multiples (slot and entry offsets) are formed where used, not held across the loop
+    StagedInbox inl = in;
+#if SCG_STAGED_OPAQUE_STRIDE
+    g.stride = sc_opaque_val(g.stride);
+    g.hstride = sc_opaque_val(g.hstride);
+    inl.stride = sc_opaque_val(inl.stride);
+#endif
     int a_i = 0, lt_i = 0;
-    for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, in, ltc, act, t, i, p, a_i, lt_i, out, scg_acc_);
-    if (!StagedInbox::kClearInAct && !nd.last_level) in.clear(c, i);
+    for (int p = 0; p < c.P; ++p) sc_staged_heap(c, g, lh, inl, ltc, act, t, i, p, a_i, lt_i, out, scg_acc_);
+    if (!StagedInbox::kClearInAct && !nd.last_level) inl.clear(c, i);
     SCG_ACC(7);
-    total = np_add(total, sc_node_act<MAXD, StagedInbox, true, kKindPaths>(c, g, ltc, dmc, i, act, t, in));
+    total = np_add(total, sc_node_act<MAXD, StagedInbox, true, kKindPaths>(c, g, ltc, dmc, i, act, t, inl));
     SCG_ACC(5);
     for (int p = 0; p < c.P; ++p) sc_observe_stock(c, g, i, p, out);
     SCG_ACC(6);
   }
   SCG_ACC_STORE;
   return np_neg(total).v;
+}
+
+template <int MAXD, bool kKindPaths = false, class Sink>
+__host__ __device__ inline double sc_staged_step(const ScCtx& c, ScEnv& g, const HeapView8& lh, const StagedInbox& in,
+                                                 const float* act, int t, Sink& out) {
+  return sc_staged_step_ctx<MAXD, kKindPaths>(HostCtx{c}, g, lh, in, act, t, out);
 }
 
 }  // namespace scg

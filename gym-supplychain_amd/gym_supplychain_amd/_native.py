@@ -196,6 +196,7 @@ SIGNATURES = {
                                    ctypes.c_void_p]),
     "scg_sc_draw_tables": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.c_uint32,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "scg_sc_nodes_max_blocks": (ctypes.c_int, [ctypes.c_int32]),
     "scg_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_void_p]),
     "scg_uniform_ints": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,

@@ -435,6 +435,11 @@ SCG_API int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float*
 SCG_API int scg_sc_draw_tables(const scg_sc_config* cfg, const scg_sc_state* st, uint32_t episode,
                                int32_t* demand, int32_t* leadtimes, void* stream);
 
+/* Testing hook: cap the node-parallel kernel's persistent grid at `blocks` blocks (0, the
+ * default: as many as the device holds at once), so a small batch runs several 64-env tiles
+ * per block and the next-tile prefetch runs (scg_sc_nodes.hip). Returns the previous cap. */
+SCG_API int scg_sc_nodes_max_blocks(int32_t blocks);
+
 #ifdef __cplusplus
 }
 #endif

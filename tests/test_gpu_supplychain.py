@@ -274,6 +274,54 @@ def test_level_kernel_equals_lane_kernel(scenario, kw):
         e.check_errors()
 
 
+@pytest.mark.parametrize("max_blocks", [2, 3, 0])
+@pytest.mark.parametrize("n_envs", [324, 322])
+@pytest.mark.parametrize("scenario,kw", [
+    ("sc-2perstage-v0", dict(total_time_steps=12, stochastic_leadtimes=True, avg_leadtime=2, max_leadtime=4)),
+    ("sc-2perstage-multiproduct-v0", dict(total_time_steps=9, build_info=True, obs_dtype=torch.float32)),
+    ("sc-2perstage-v0", dict(total_time_steps=7, serial=True))])
+def test_nodes_kernel_persistent_tiles_equal_lane_kernel(scenario, kw, n_envs, max_blocks):
+    """The node-parallel kernel's persistent grid (scg_sc_nodes_max_blocks caps it, so a
+    block steps several 64-env tiles and prefetches the next tile's heaps, sizes and stocks
+    by LDS-DMA while its last phases run) against the lane kernel over every env, two
+    episodes with auto-reset: N = 324 takes the DMA stage with a 4-env tail tile, N = 322
+    the register stage; stochastic lead times, two products with ledgers, and every env on
+    the serial walk (no prefetch) — identical obs, rewards, returns, stocks and ledgers."""
+    import gym_supplychain_amd as gsa
+    from gym_supplychain_amd import _native as nat
+    kw = dict(kw)
+    serial = kw.pop("serial", False)
+    kw.setdefault("obs_dtype", torch.float64)  # the two-product block fits LDS with float32 observations
+    envs = [gsa.make_vec(scenario, n_envs, seed=5, device=DEV, kernel=k, **kw)
+            for k in ("lane", "nodes")]
+    assert envs[1].kernel == "nodes"
+    if serial:
+        envs[1]._flags |= nat.SCG_SC_SERIAL
+    prev = nat.lib.scg_sc_nodes_max_blocks(max_blocks)
+    try:
+        o = [e.reset() for e in envs]
+        assert torch.equal(o[0], o[1])
+        gen = torch.Generator(device=DEV).manual_seed(11)
+        T = envs[0].spec.total_time_steps
+        for t in range(2 * T):
+            a = torch.rand((n_envs, envs[0].n_actions), generator=gen, device=DEV) * 2.4 - 1.2
+            (o0, r0, d0, i0), (o1, r1, d1, i1) = (e.step(a) for e in envs)
+            assert torch.equal(o0, o1) and torch.equal(r0, r1) and torch.equal(d0, d1), t
+            assert torch.equal(envs[0].stock, envs[1].stock), t
+            assert torch.equal(envs[0]._heap_size, envs[1]._heap_size), t  # both env-fastest
+            if envs[0].build_info:
+                assert torch.equal(envs[0]._led, envs[1]._led) and torch.equal(envs[0]._led_k, envs[1]._led_k), t
+            if "terminal_observation" in i0:
+                assert torch.equal(i0["terminal_observation"], i1["terminal_observation"])
+                assert torch.equal(i0["episode_return"], i1["episode_return"])
+        for n in (0, 100, n_envs - 1):
+            assert envs[0].heaps(n) == envs[1].heaps(n)
+    finally:
+        nat.lib.scg_sc_nodes_max_blocks(prev)
+    for e in envs:
+        e.check_errors()
+
+
 @pytest.mark.parametrize("kernel", ["lane", "staged", "nodes"])
 @pytest.mark.parametrize("name", CASES)
 def test_ledgers_match_reference(name, kernel):

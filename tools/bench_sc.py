@@ -147,7 +147,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "level", "staged", "nodes", "all", "both"])
     ap.add_argument("--build-info", action="store_true", help="keep the build_info ledgers (info['sc_episode'])")
+    ap.add_argument("--nodes-max-blocks", type=int, default=0,
+                    help="cap the node-parallel kernel's persistent grid (scg_sc_nodes_max_blocks; experiments)")
     a = ap.parse_args()
+    if a.nodes_max_blocks:
+        from gym_supplychain_amd import _native as nat
+        nat.lib.scg_sc_nodes_max_blocks(a.nodes_max_blocks)
     names = {"both": ["2perstage", "ntom"], "all": ["2perstage", "2perstage_mp", "ntom"]}.get(a.scenario, [a.scenario])
     for name in names:
         kernels = [a.kernel]
