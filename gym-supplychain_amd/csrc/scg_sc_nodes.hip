@@ -202,7 +202,9 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     const ScArgs& a = *(const ScArgs*)ap;
     const ScCtx& c = a.c;
     const int NN = c.n_nodes, P = c.P, NP = NN * P, H = c.H;
-    const int Ap = c.A | 1, Op = c.O | 1;  // odd row strides: lanes hit distinct banks
+    // odd row strides: lanes hit distinct banks; the action tile unpadded when the LDS-DMA
+    // prefetch may fill it (one contiguous span of the batch's env-major action rows)
+    const int Ap = dma && SCG_NODES_PREFETCH ? c.A : c.A | 1, Op = c.O | 1;
     double* hval = reinterpret_cast<double*>(smem);
     double* sbuf0 = hval + static_cast<int64_t>(NP) * H * 64;  // two [NP][64] buffers: stocks / released sums
     double* ibval = sbuf0 + NP * 64;
@@ -258,7 +260,14 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     // a round more for a longer heap); nothing is waited for until all are in flight. Then
     // the actions to their LDS tile and what each heap releases.
     bool bad = false;
-    {
+    if (prefetched) {  // everything came by LDS-DMA while the previous tile finished
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int i = w; i < NN; i += W)
+        for (int p = 0; p < P; ++p) {
+          const int hp = i * P + p;
+          if (live) bad |= !sc_recv_scan(lheap(hp), hsz[hp * 64 + lane], a.t, recv[hp * 64 + lane]);
+        }
+    } else {
       constexpr int kAct = 4;  // action elements per thread per round
       const float* src = a.act + n0 * c.A;
       const int na = nb * c.A;
@@ -267,11 +276,10 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
       for (int u = 0; u < kAct; ++u)
         if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
       const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
-      if (prefetched || (dma && SCG_NODES_DMA_FIRST)) {
-        if (!prefetched)
-          for (int i = w; i < NN; i += W)
-            for (int p = 0; p < P; ++p) nodes_dma_heap(a, i * P + p, H, n0, nb, lane, htk, hval, hsz, stk);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs (this tile's or the prefetch) have landed
+      if (dma && SCG_NODES_DMA_FIRST) {
+        for (int i = w; i < NN; i += W)
+          for (int p = 0; p < P; ++p) nodes_dma_heap(a, i * P + p, H, n0, nb, lane, htk, hval, hsz, stk);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         for (int i = w; i < NN; i += W)
           for (int p = 0; p < P; ++p) {
             const int hp = i * P + p;
@@ -417,6 +425,18 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     else
       barrier_lds_only();
     NSTAMP(7);
+    if (pf) {  // every wave is past its last read of the action tile and wave 0 of ret0: the
+               // next tile's action span (1 KiB per wave instruction, the waves in turn) and
+               // episode returns come by LDS-DMA while this tile's observations go out
+      const int bytes = nnb * c.A * 4;
+      const char* src = reinterpret_cast<const char*>(a.act + nn0 * c.A);
+      for (int k = w; k * 1024 < bytes; k += W) {
+        const int off = k * 1024 + lane * 16;
+        if (off < bytes) glds16(src + off, reinterpret_cast<char*>(act_t) + k * 1024);
+      }
+      if (w == 0 && a.ep_ret)
+        glds_rows<512>(reinterpret_cast<const char*>(a.ep_ret + nn0), 0, reinterpret_cast<char*>(ret0), 1, lane, nnb);
+    }
 
 #if !SCG_NODES_LED_EARLY
     if (ledgers && live) ledger_entries(w, W);

@@ -209,8 +209,10 @@ __global__ __launch_bounds__(EPB) void sc_step_lds_kernel(const ScArgs a) {
 #endif
 // LED: build_info ledgers kept (a separate instantiation: without it every ledger note,
 // and the per-destination unit sums only ledgers read, compile away).
+// The staged kernel's context re-read per node (KernargCtx): 249 -> 199 VGPRs and a third of
+// the SGPR spill reloads, yet 2.3 % slower on ntom (3.97 -> 4.07 ms, profiles/r05e_*), so off.
 #ifndef SCG_STAGED_KARG_CTX
-#define SCG_STAGED_KARG_CTX 1
+#define SCG_STAGED_KARG_CTX 0
 #endif
 template <int MAXD, bool LED>
 __global__ __launch_bounds__(kScBlock)
