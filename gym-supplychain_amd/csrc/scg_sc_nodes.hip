@@ -20,6 +20,10 @@
 //                                                                             | barrier
 //   out    (every thread)       the observation tile -> HBM, one contiguous span per block;
 //                               wave 0 resets its envs at an auto-reset step
+// The grid is persistent: as many blocks as the device holds at once (two per CU), each
+// stepping tiles of 64 envs in turn, with the launch arguments re-read per tile through a
+// pointer the compiler cannot carry across tiles (nothing derived from them is held, or
+// spilled, across the loop).
 // An env any wave flagged skips act and heaps; wave 0 steps it alone on its staged heaps,
 // node after node in the reference's order (sc_nodes_serial). Observations and actions go
 // through LDS tiles so HBM sees whole rows; the state pointers stay the batch's base
@@ -99,100 +103,29 @@ struct TileWalk {
 #ifndef SCG_NODES_WPE
 #define SCG_NODES_WPE 4
 #endif
-// LDS-DMA (gfx950 global_load_lds_dwordx4): this lane's 16 bytes at `src` land at
-// lds_base + 16 * lane, lds_base wave-uniform; no VGPR holds the data, the wave's vmcnt
-// counts it.
-typedef __attribute__((address_space(3))) void* LdsPtr;
-typedef __attribute__((address_space(1))) void* GblPtr;
-__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
-  __builtin_amdgcn_global_load_lds((GblPtr)(const_cast<void*>(src)), (LdsPtr)(lds_base), 16, 0, 0);
-}
-
-// Rows [0, nrows) of a block's 64-env slab by LDS-DMA: global row r at src + r * gstride
-// bytes (the block's first env), LDS row r at dst + r * kRowBytes (256: int32 per env, 512:
-// double per env), 16 bytes per lane, 4 or 2 rows per wave instruction. Lanes whose bytes
-// lie past the block's `nb` envs read the row's first bytes instead (never used), so no lane
-// reads past the batch; nb is a multiple of 4 (scg_sc_step takes this path for N % 4 == 0).
-template <int kRowBytes>
-__device__ __forceinline__ void glds_rows(const char* src, int64_t gstride, char* dst, int nrows, int lane, int nb) {
-  constexpr int kLanesPerRow = kRowBytes / 16, kRowsPerInst = 64 / kLanesPerRow;
-  constexpr int kElem = kRowBytes / 64;  // bytes per env
-  const int col = (lane % kLanesPerRow) * 16;
-  const int c = col < nb * kElem ? col : 0;
-  for (int r0 = 0; r0 < nrows; r0 += kRowsPerInst) {  // wave-uniform
-    const int r = r0 + lane / kLanesPerRow;
-    if (r < nrows) glds16(src + r * gstride + c, dst + r0 * kRowBytes);
-  }
-}
-
-// Everything heap (i, p) and its stock need from HBM for a block's stage, by LDS-DMA in one
-// memory round: every heap slot (times and amounts), the size and the stock rows.
-__device__ __forceinline__ void nodes_dma_heap(const ScArgs& a, int hp, int H, int64_t n0, int nb, int lane,
-                                               int32_t* htk, double* hval, int32_t* hsz, double* stk) {
-  const int64_t N = a.n;
-  glds_rows<256>(reinterpret_cast<const char*>(a.tk + static_cast<int64_t>(hp) * H * N + n0), N * 4,
-                 reinterpret_cast<char*>(htk + hp * H * 64), H, lane, nb);
-  glds_rows<512>(reinterpret_cast<const char*>(a.val + static_cast<int64_t>(hp) * H * N + n0), N * 8,
-                 reinterpret_cast<char*>(hval + hp * H * 64), H, lane, nb);
-  glds_rows<256>(reinterpret_cast<const char*>(a.size + hp * N + n0), 0, reinterpret_cast<char*>(hsz + hp * 64), 1,
-                 lane, nb);
-  glds_rows<512>(reinterpret_cast<const char*>(a.stock + hp * N + n0), 0, reinterpret_cast<char*>(stk + hp * 64), 1,
-                 lane, nb);
-}
-
-// The block barrier while LDS-DMAs may be in flight: LDS writes made visible, memory
-// operations left outstanding (__syncthreads would wait for the DMAs too).
-__device__ __forceinline__ void barrier_lds_only() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-#ifndef SCG_NODES_PREFETCH
-#define SCG_NODES_PREFETCH 1
-#endif
-#ifndef SCG_NODES_LAUNDER
-#define SCG_NODES_LAUNDER 1
-#endif
-#ifndef SCG_NODES_DMA
-#define SCG_NODES_DMA 1
-#endif
-// The first tile of a block by LDS-DMA too (1) or by register loads (0: measured faster,
-// 37.6 against 40.4 us with no prefetch, profiles/r05c_nodes_persistent_ab.log); the
-// prefetched tiles always come by LDS-DMA.
-#ifndef SCG_NODES_DMA_FIRST
-#define SCG_NODES_DMA_FIRST 0
-#endif
-
 // Four waves per SIMD (<= 128 VGPRs): two blocks of eight waves per CU, which is also what
 // their LDS allows.
 // F64: float64 observations; LED: build_info ledgers (a separate instantiation, so the
 // ledger code costs the common run nothing).
-// Persistent: block b steps tiles b, b + gridDim.x, ... (64 envs each; the launch sizes the
+// Persistent: block b steps tiles b, b + gridDim.x, ... (64 envs each); the launch sizes the
 // grid to the blocks the device holds at once, so the second round of tiles needs no new
-// blocks). dma (N % 4 == 0): heaps, sizes and stocks arrive by LDS-DMA in one memory round,
-// and while a tile's last phases run, each wave's DMA brings the next tile's heaps, sizes and
-// stocks of its nodes into the LDS its nodes just released (the stocks into the other of two
-// stock buffers), so the next tile's stage waits only for its action rows.
+// blocks and each block's next tile follows its last without a dispatch.
 template <int MAXD, bool F64, bool LED>
 __global__ __launch_bounds__(64 * kNodesMaxWaves) __attribute__((amdgpu_waves_per_eu(SCG_NODES_WPE)))
-void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
+void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
   using ObsT = typename std::conditional<F64, double, float>::type;
   extern __shared__ __align__(16) unsigned char smem[];
   // the wave index is wave-uniform: said so, node records are read with scalar loads
   const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_tiles = (a_arg.n + 63) / 64;
   constexpr bool ledgers = LED;
-  // a tile's stocks and released sums take the two [NP][64] buffers in turn when the next
-  // tile's stocks were prefetched into the released-sum buffer
-  bool swapped = false, prefetched = false;
 
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     // the lane index, opaque to the compiler inside each tile: the per-lane LDS and HBM
     // addresses derived from it are computed where used, not hoisted out of the tile loop
     // and held in registers across it (which spilled the kernel at its 128-VGPR budget)
-#if SCG_NODES_LAUNDER
     int lane;
     asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
-#else
-    const int lane = lane0;
-#endif
     // the launch arguments through a pointer the compiler cannot see across tiles: each tile
     // reads them (scalar loads) and derives its addresses itself, instead of every derived
     // value being hoisted out of the loop and held in scalar registers across it
@@ -202,15 +135,13 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     const ScArgs& a = *(const ScArgs*)ap;
     const ScCtx& c = a.c;
     const int NN = c.n_nodes, P = c.P, NP = NN * P, H = c.H;
-    // odd row strides: lanes hit distinct banks; the action tile unpadded when the LDS-DMA
-    // prefetch may fill it (one contiguous span of the batch's env-major action rows)
-    const int Ap = dma && SCG_NODES_PREFETCH ? c.A : c.A | 1, Op = c.O | 1;
+    const int Ap = c.A | 1, Op = c.O | 1;  // odd row strides: lanes hit distinct banks
     double* hval = reinterpret_cast<double*>(smem);
-    double* sbuf0 = hval + static_cast<int64_t>(NP) * H * 64;  // two [NP][64] buffers: stocks / released sums
-    double* ibval = sbuf0 + NP * 64;
+    double* recv = hval + static_cast<int64_t>(NP) * H * 64;  // released sums [NP][64]
+    double* ibval = recv + NP * 64;
     double* cost_v = ibval + static_cast<int64_t>(E) * 64;
-    double* sbuf1 = cost_v + NN * 64;
-    double* ret0 = sbuf1 + NP * 64;  // episode returns [64] (wave 0's prefetch)
+    double* stk = cost_v + NN * 64;  // the tile's stocks [NP][64] for the step
+    double* ret0 = stk + NP * 64;    // episode returns [64] (wave 0's prefetch)
     ObsT* obs_t = reinterpret_cast<ObsT*>(ret0 + 64);
     int32_t* htk = reinterpret_cast<int32_t*>(obs_t + 64 * Op);
     int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
@@ -219,8 +150,6 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     int32_t* amb = cost_k + NN * 64;
     uint64_t* lword = reinterpret_cast<uint64_t*>(amb + W * 64);  // ledger entry marks and types [NP][64]
     float* act_t = reinterpret_cast<float*>(lword + NP * 64);
-    double* const stk = swapped ? sbuf0 : sbuf1;
-    double* const recv = swapped ? sbuf1 : sbuf0;
     const bool terminal = a.flags & 1;
     const bool autoreset = a.flags & 2;
     const int64_t n0 = tile * 64;
@@ -238,14 +167,6 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
       g.led_word = lword + lane;
       g.led_word_stride = 64;
     }
-#ifdef SCG_NODES_STAGGER_US
-    // experiment only: blocks [LO, HI) start late, so co-resident blocks run offset phases
-    if (tile == blockIdx.x && blockIdx.x >= SCG_NODES_STAGGER_LO && blockIdx.x < SCG_NODES_STAGGER_HI) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-      while (__builtin_amdgcn_s_memrealtime() - t0 < static_cast<uint64_t>(SCG_NODES_STAGGER_US * 100))
-        __builtin_amdgcn_s_sleep(8);
-    }
-#endif
     NSTAMP(0);
 
     // the step's observation row, whichever buffer(s) it goes to (chosen at the copy-out)
@@ -255,19 +176,11 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     const float* act = act_t + lane * Ap;
 
     // stage, one memory round: every thread requests its share of the tile's action rows
-    // (one contiguous span), wave 0 the episode returns, every wave its nodes' heaps, sizes
-    // and stocks (LDS-DMA, unless the previous tile prefetched them; else register loads and
-    // a round more for a longer heap); nothing is waited for until all are in flight. Then
-    // the actions to their LDS tile and what each heap releases.
+    // (one contiguous span), every wave its node's stocks, heap sizes and the first kStage
+    // slots of each heap, wave 0 the episode returns; nothing is waited for until all are in
+    // flight. Then everything to LDS, the rest of a longer heap, and what each heap releases.
     bool bad = false;
-    if (prefetched) {  // everything came by LDS-DMA while the previous tile finished
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (int i = w; i < NN; i += W)
-        for (int p = 0; p < P; ++p) {
-          const int hp = i * P + p;
-          if (live) bad |= !sc_recv_scan(lheap(hp), hsz[hp * 64 + lane], a.t, recv[hp * 64 + lane]);
-        }
-    } else {
+    {
       constexpr int kAct = 4;  // action elements per thread per round
       const float* src = a.act + n0 * c.A;
       const int na = nb * c.A;
@@ -276,34 +189,23 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
       for (int u = 0; u < kAct; ++u)
         if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
       const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
-      if (dma && SCG_NODES_DMA_FIRST) {
-        for (int i = w; i < NN; i += W)
-          for (int p = 0; p < P; ++p) nodes_dma_heap(a, i * P + p, H, n0, nb, lane, htk, hval, hsz, stk);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (int i = w; i < NN; i += W)
-          for (int p = 0; p < P; ++p) {
-            const int hp = i * P + p;
-            if (live) bad |= !sc_recv_scan(lheap(hp), hsz[hp * 64 + lane], a.t, recv[hp * 64 + lane]);
-          }
-      } else {
-        for (int i = w; i < NN; i += W)
-          for (int p = 0; p < P; ++p) {
-            const int hp = i * P + p;
-            if (!live) continue;
-            const int64_t r = static_cast<int64_t>(hp) * a.n + n;
-            const double st = a.stock[r];
-            const int32_t sz = a.size[r];
-            stk[hp * 64 + lane] = st;
-            hsz[hp * 64 + lane] = sz;
-            const HeapView lh = lheap(hp);
-            // the heap's first slots are requested with the size (sc_nodes_copy_heap, shared
-            // with the host harness); a longer heap costs a round more
-            sc_nodes_copy_heap(HeapView{a.tk + static_cast<int64_t>(hp) * H * a.n + n,
-                                        a.val + static_cast<int64_t>(hp) * H * a.n + n, a.n},
-                               lh, H, sz);
-            bad |= !sc_recv_scan(lh, sz, a.t, recv[hp * 64 + lane]);
-          }
-      }
+      for (int i = w; i < NN; i += W)
+        for (int p = 0; p < P; ++p) {
+          const int hp = i * P + p;
+          if (!live) continue;
+          const int64_t r = static_cast<int64_t>(hp) * a.n + n;
+          const double st = a.stock[r];
+          const int32_t sz = a.size[r];
+          stk[hp * 64 + lane] = st;
+          hsz[hp * 64 + lane] = sz;
+          const HeapView lh = lheap(hp);
+          // the heap's first slots are requested with the size (sc_nodes_copy_heap, shared
+          // with the host harness); a longer heap costs a round more
+          sc_nodes_copy_heap(HeapView{a.tk + static_cast<int64_t>(hp) * H * a.n + n,
+                                      a.val + static_cast<int64_t>(hp) * H * a.n + n, a.n},
+                             lh, H, sz);
+          bad |= !sc_recv_scan(lh, sz, a.t, recv[hp * 64 + lane]);
+        }
       {
         TileWalk tw(threadIdx.x, blockDim.x, c.A);
 #pragma unroll
@@ -320,14 +222,6 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     bool flagged = (a.flags & 4) != 0;
     for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
     const bool go = live && !flagged;
-    // the next tile's heaps, sizes and stocks come by LDS-DMA as this tile's heaps finish
-    // (every wave reads the same flags: the decision is block-uniform). Not when an env of
-    // this tile steps serially (wave 0 reads every node's staged heaps after the heaps
-    // phase) or resets (the reset writes this tile's heaps).
-    const bool pf = SCG_NODES_PREFETCH && dma && tile + gridDim.x < n_tiles && !autoreset &&
-                    __builtin_amdgcn_ballot_w64(flagged) == 0;
-    const int64_t nn0 = (tile + gridDim.x) * 64;
-    const int nnb = pf ? (a.n - nn0 < 64 ? static_cast<int>(a.n - nn0) : 64) : 0;
 
     // act: every node at once (a node's act needs only what its own heaps release)
     if (go)
@@ -341,8 +235,7 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
     __syncthreads();
     NSTAMP(2);
 
-    // heaps; then the next tile's DMA into what this wave's nodes released (the released
-    // sums are dead since the act: the next stocks go there)
+    // heaps
     if (go)
       for (int i = w; i < NN; i += W) {
         WordCache ltc{0, U4{0, 0, 0, 0}, false};
@@ -352,11 +245,6 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
           sc_nodes_heap(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, a.t, i, p, a_i, lt_i, sink);
         }
       }
-    if (pf) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of its heaps are done
-      for (int i = w; i < NN; i += W)
-        for (int p = 0; p < P; ++p) nodes_dma_heap(a, i * P + p, H, nn0, nnb, lane, htk, hval, hsz, recv);
-    }
     NSTAMP(3);
 
     // ledgers: entry q of an env, the nodes' entries added in node order (:750-760); at an
@@ -418,25 +306,8 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
       for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, a.t, k, sink);  // (:771)
       sc_observe_tail(c, a.t, sink);                                               // (:786)
     }
-    // an auto-reset below writes this tile's heaps in HBM after every wave's copy-back
-    // (__syncthreads waits for the stores); else the prefetch may stay in flight
-    if (autoreset)
-      __syncthreads();
-    else
-      barrier_lds_only();
+    __syncthreads();
     NSTAMP(7);
-    if (pf) {  // every wave is past its last read of the action tile and wave 0 of ret0: the
-               // next tile's action span (1 KiB per wave instruction, the waves in turn) and
-               // episode returns come by LDS-DMA while this tile's observations go out
-      const int bytes = nnb * c.A * 4;
-      const char* src = reinterpret_cast<const char*>(a.act + nn0 * c.A);
-      for (int k = w; k * 1024 < bytes; k += W) {
-        const int off = k * 1024 + lane * 16;
-        if (off < bytes) glds16(src + off, reinterpret_cast<char*>(act_t) + k * 1024);
-      }
-      if (w == 0 && a.ep_ret)
-        glds_rows<512>(reinterpret_cast<const char*>(a.ep_ret + nn0), 0, reinterpret_cast<char*>(ret0), 1, lane, nnb);
-    }
 
 #if !SCG_NODES_LED_EARLY
     if (ledgers && live) ledger_entries(w, W);
@@ -463,17 +334,15 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E, int dma) {
       __syncthreads();
     }
     if (live) {  // the stocks of this wave's nodes back, one 64-env row per instruction (the
-                 // next tile's stage rewrites these rows of the buffers: the same wave)
+                 // next tile's stage rewrites these rows: the same wave)
       for (int i = w; i < NN; i += W)
         for (int p = 0; p < P; ++p) a.stock[(i * P + p) * a.n + n] = stk[(i * P + p) * 64 + lane];
       if (g.overflow) atomicOr(a.err, 1);
     }
     NSTAMP(4);
-    // the next tile: its stocks in the released-sum buffer when prefetched; the buffers the
-    // out phase still reads (the observation tile, this tile's stocks) are next written after
-    // the next tile's first barrier
-    swapped ^= pf;
-    prefetched = pf;
+    // the next tile's stage rewrites the action tile, ret0 and, per wave, only the stock, size
+    // and heap rows of its own nodes (whose stocks it copied back just above); the rows other
+    // waves read (the observation tile) are next written after that tile's first barrier
   }
 }
 
@@ -551,16 +420,16 @@ int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
   }
   const int64_t tiles = (a.n + 63) / 64;
   int64_t blocks = tiles;
-  if (SCG_NODES_PERSISTENT) {
+  // the ledger instantiation keeps one block per tile (persistent measured 55.4 -> 56.7 us,
+  // profiles/r05f_nodes_persistent_ab.log)
+  if (SCG_NODES_PERSISTENT && !LED) {
     const int64_t resident = sc_nodes_resident_blocks<MAXD, F64, LED>(dev, W, lds);
     if (resident > 0 && resident < tiles) blocks = resident;
   }
   const int cap = g_nodes_max_blocks.load(std::memory_order_relaxed);
   if (cap > 0 && cap < blocks) blocks = cap;
-  // the LDS-DMA stage reads whole 16-byte groups of a 64-env row: the batch a multiple of 4
-  const int dma = SCG_NODES_DMA && a.n % 4 == 0 ? 1 : 0;
   hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_step_nodes_kernel<MAXD, F64, LED>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(64 * W), lds, s, a, W, E, dma);
+                     dim3(64 * W), lds, s, a, W, E);
   return check_launch("sc_step_nodes_kernel");
 }
 

@@ -282,11 +282,10 @@ def test_level_kernel_equals_lane_kernel(scenario, kw):
     ("sc-2perstage-v0", dict(total_time_steps=7, serial=True))])
 def test_nodes_kernel_persistent_tiles_equal_lane_kernel(scenario, kw, n_envs, max_blocks):
     """The node-parallel kernel's persistent grid (scg_sc_nodes_max_blocks caps it, so a
-    block steps several 64-env tiles and prefetches the next tile's heaps, sizes and stocks
-    by LDS-DMA while its last phases run) against the lane kernel over every env, two
-    episodes with auto-reset: N = 324 takes the DMA stage with a 4-env tail tile, N = 322
-    the register stage; stochastic lead times, two products with ledgers, and every env on
-    the serial walk (no prefetch) — identical obs, rewards, returns, stocks and ledgers."""
+    block steps several 64-env tiles in turn) against the lane kernel over every env, two
+    episodes with auto-reset, with a 4- or 2-env tail tile; stochastic lead times, two
+    products with ledgers (that instantiation keeps one block per tile), and every env on
+    the serial walk — identical obs, rewards, returns, stocks, heaps and ledgers."""
     import gym_supplychain_amd as gsa
     from gym_supplychain_amd import _native as nat
     kw = dict(kw)
