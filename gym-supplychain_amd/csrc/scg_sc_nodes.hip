@@ -103,6 +103,13 @@ struct TileWalk {
 #ifndef SCG_NODES_WPE
 #define SCG_NODES_WPE 4
 #endif
+// Streaming (non-temporal) stores for the rows a step writes once and only the next step
+// reads (heap copy-back, stocks, observations): 0 off, 1 the ledger instantiation only, 2
+// every instantiation (sc-2perstage 37.4 -> 36.7 us; the ledger run within noise,
+// profiles/r05j_nodes_nt_ab.log).
+#ifndef SCG_NODES_NT
+#define SCG_NODES_NT 2
+#endif
 // Four waves per SIMD (<= 128 VGPRs): two blocks of eight waves per CU, which is also what
 // their LDS allows.
 // F64: float64 observations; LED: build_info ledgers (a separate instantiation, so the
@@ -119,6 +126,8 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
   const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_tiles = (a_arg.n + 63) / 64;
   constexpr bool ledgers = LED;
+  // streaming stores for the heap copy-back and the observation and stock rows (SCG_NODES_NT)
+  constexpr bool kStream = SCG_NODES_NT == 2 || (SCG_NODES_NT == 1 && LED);
 
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     // the lane index, opaque to the compiler inside each tile: the per-lane LDS and HBM
@@ -242,7 +251,7 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
         int a_i = 0, lt_i = 0;
         for (int p = 0; p < P; ++p) {
           const int hp = i * P + p;
-          sc_nodes_heap(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, a.t, i, p, a_i, lt_i, sink);
+          sc_nodes_heap<kStream>(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, a.t, i, p, a_i, lt_i, sink);
         }
       }
     NSTAMP(3);
@@ -320,8 +329,13 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
     TileWalk tw(threadIdx.x, blockDim.x, c.O);
     for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
       const ObsT x = obs_t[tw.r * Op + tw.k];
-      if (dst0) dst0[n0 * c.O + q] = x;
-      if (dst1) dst1[n0 * c.O + q] = x;
+      if constexpr (kStream) {
+        if (dst0) __builtin_nontemporal_store(x, &dst0[n0 * c.O + q]);
+        if (dst1) __builtin_nontemporal_store(x, &dst1[n0 * c.O + q]);
+      } else {
+        if (dst0) dst0[n0 * c.O + q] = x;
+        if (dst1) dst1[n0 * c.O + q] = x;
+      }
     }
     if (autoreset) {  // after the barrier every wave's heap copy-back has landed
       if (w == 0 && live) {
@@ -336,7 +350,12 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
     if (live) {  // the stocks of this wave's nodes back, one 64-env row per instruction (the
                  // next tile's stage rewrites these rows: the same wave)
       for (int i = w; i < NN; i += W)
-        for (int p = 0; p < P; ++p) a.stock[(i * P + p) * a.n + n] = stk[(i * P + p) * 64 + lane];
+        for (int p = 0; p < P; ++p) {
+          if constexpr (kStream)
+            __builtin_nontemporal_store(stk[(i * P + p) * 64 + lane], &a.stock[(i * P + p) * a.n + n]);
+          else
+            a.stock[(i * P + p) * a.n + n] = stk[(i * P + p) * 64 + lane];
+        }
       if (g.overflow) atomicOr(a.err, 1);
     }
     NSTAMP(4);
@@ -403,6 +422,10 @@ int64_t sc_nodes_resident_blocks(int dev, int W, size_t lds) {
 #define SCG_NODES_PERSISTENT 1
 #endif
 
+#ifndef SCG_NODES_LED_PERSISTENT
+#define SCG_NODES_LED_PERSISTENT 0
+#endif
+
 std::atomic<int> g_nodes_max_blocks{0};  // scg_sc_nodes_max_blocks (tests)
 
 template <int MAXD, bool F64, bool LED>
@@ -422,7 +445,7 @@ int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
   int64_t blocks = tiles;
   // the ledger instantiation keeps one block per tile (persistent measured 55.4 -> 56.7 us,
   // profiles/r05f_nodes_persistent_ab.log)
-  if (SCG_NODES_PERSISTENT && !LED) {
+  if (SCG_NODES_PERSISTENT && (!LED || SCG_NODES_LED_PERSISTENT)) {
     const int64_t resident = sc_nodes_resident_blocks<MAXD, F64, LED>(dev, W, lds);
     if (resident > 0 && resident < tiles) blocks = resident;
   }

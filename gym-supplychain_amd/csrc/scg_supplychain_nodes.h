@@ -158,7 +158,9 @@ __host__ __device__ inline Num sc_nodes_act(const ScCtx& c, ScEnv& g, const Node
 // advances them, :243-259) — then its in-transit bins and the copy back to the env's state.
 // The popped sum went into the stock already (sc_nodes_act), unless `receive`: then it is
 // added here (:225-228), as the serial walk below needs.
-template <class Sink>
+// kStream (device): the copy back with non-temporal stores (written once per step, read
+// next step: evict-first in the caches, so they do not push out what this step reads again).
+template <bool kStream = false, class Sink>
 __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const HeapView& lh, int32_t& sz,
                                               const NodesInbox& in, WordCache& ltc, const float* act, int t, int i,
                                               int p, int& a_i, int& lt_i, Sink& out, bool receive = false) {
@@ -185,7 +187,16 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
     }
   }
   const HeapView gh = sc_heap(c, g, i, p);
-  sc_observe_bins(c, lh, sz, t, i, p, out, [&](int k, const HeapEntry& e) { gh.put(k, e); });  // copy back
+  sc_observe_bins(c, lh, sz, t, i, p, out, [&](int k, const HeapEntry& e) {  // copy back
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (kStream) {
+      __builtin_nontemporal_store(e.tk, &gh.tk[k * gh.stride]);
+      __builtin_nontemporal_store(e.v, &gh.val[k * gh.stride]);
+      return;
+    }
+#endif
+    gh.put(k, e);
+  });
   sc_size(c, g, i, p) = sz;
 }
 
