@@ -89,7 +89,9 @@ def main():
         for s_ in build_native.SOURCES:
             obj = os.path.splitext(s_)[0] + ".o"
             tobj = os.path.join(tree_objs, obj)
-            text = open(os.path.join(csrc, s_)).read()
+            # a macro named by the source or by any header counts (headers reach every source)
+            text = open(os.path.join(csrc, s_)).read() + "".join(
+                open(os.path.join(csrc, h)).read() for h in os.listdir(csrc) if h.endswith(".h"))
             fresh = os.path.exists(tobj) and os.path.getmtime(tobj) >= os.path.getmtime(os.path.join(tree_csrc, s_))
             if headers_same and same(s_) and fresh and not any(m in text for m in macros):
                 shutil.copyfile(os.path.join(tree_objs, obj), os.path.join(out + ".objs", obj))  # fresh mtime
