@@ -36,6 +36,34 @@
 #include <vector>
 
 #include "scg_common.h"
+#if defined(SCG_NODES_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+// Diagnostic build only: every stamp (the phase boundaries NSTAMP below, and the end of each
+// section of the act and heaps phases, SCG_ACCP(ptr, k) in scg_supplychain_core.h / _nodes.h)
+// goes to the wave's slots in a static LDS array, and lane 0 copies them to HBM once, at the
+// tile's end: a global store per stamp would make the next wait on the vector memory counter
+// (loads and stores share it on gfx950) sit out that store's latency.
+// LDS slots per wave: 0-7 phase stamps, 8 real-time clock at the start, 9 + j section j
+// (sections k = 0..3 -> j = k, k = 7..13 -> j = k - 3).
+constexpr int kNLdsSlots = 20;
+__shared__ unsigned long long s_nodes_stamps[8 * kNLdsSlots];
+#define SCG_STAMP(k)
+#define SCG_ACC_DECL
+#define SCG_ACC(k)
+#define SCG_ACC_STORE
+namespace scg {
+struct ScAcc {  // a marker: a non-null ScEnv::dbg turns the section stamps on
+  int unused;
+};
+}  // namespace scg
+#define SCG_ACCP(ptr, k)                                                                              \
+  do {                                                                                                \
+    if (ptr) {                                                                                        \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();                                   \
+      if ((threadIdx.x & 63u) == 0)                                                                   \
+        s_nodes_stamps[(threadIdx.x / 64u) * kNLdsSlots + 9 + ((k) < 4 ? (k) : (k) - 3)] = now_;      \
+    }                                                                                                 \
+  } while (0)
+#endif
 #include "scg_supplychain_core.h"
 #include "scg_supplychain_args.h"
 #include "scg_supplychain_nodes.h"
@@ -45,27 +73,38 @@
 // barrier, 1 acted, 2 past the second, 3 heaps done, 7 past the third, 4 end) into a buffer of its own that scg_nodes_debug_stamps copies
 // out; nothing else reads it. In the product build NSTAMP is empty.
 #ifdef SCG_NODES_STAMPS
-// Slots 8 and 9 hold the real-time clock (100 MHz, one clock for the chip) at start and end,
-// 10 and 11 the wave's HW_ID and XCC_ID registers (where the block was placed).
-constexpr int kNStampSlots = 12;
+// Global record per wave: slots 0-7 the phase stamps, 8 and 9 the real-time clock (100 MHz,
+// one clock for the chip) at start and end, 10 and 11 the wave's HW_ID and XCC_ID registers
+// (where the block was placed), 12 + k the end of section k of the act and heaps phases.
+constexpr int kNStampSlots = 28;
 constexpr int kNStampWaves = 1 << 14;
 __device__ unsigned long long g_nodes_stamps[kNStampWaves * kNStampSlots];
+#if defined(__HIP_DEVICE_COMPILE__)
 #define NSTAMP(k)                                                                                   \
   do {                                                                                              \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                                   \
-    const unsigned long long rt_ = ((k) == 0 || (k) == 4) ? __builtin_amdgcn_s_memrealtime() : 0ull; \
-    const unsigned w_ = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;                        \
-    if ((threadIdx.x & 63u) == 0 && w_ < static_cast<unsigned>(kNStampWaves)) {                     \
-      unsigned long long* s_ = g_nodes_stamps + w_ * kNStampSlots;                                  \
-      s_[(k)] = now_;                                                                               \
-      if ((k) == 0) {                                                                               \
-        s_[8] = rt_;                                                                                \
+    unsigned long long* l_ = s_nodes_stamps + (threadIdx.x / 64u) * kNLdsSlots;                     \
+    if ((threadIdx.x & 63u) == 0) {                                                                 \
+      l_[(k)] = now_;                                                                               \
+      if ((k) == 0) l_[8] = __builtin_amdgcn_s_memrealtime();                                       \
+    }                                                                                               \
+    if ((k) == 4) {                                                                                 \
+      const unsigned long long rt_ = __builtin_amdgcn_s_memrealtime();                              \
+      const unsigned w_ = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;                      \
+      if ((threadIdx.x & 63u) == 0 && w_ < static_cast<unsigned>(kNStampWaves)) {                   \
+        unsigned long long* s_ = g_nodes_stamps + w_ * kNStampSlots;                                \
+        for (int j_ = 0; j_ < 9; ++j_) s_[j_] = l_[j_];                                             \
+        s_[9] = rt_;                                                                                \
         s_[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                                         \
         s_[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20);                                        \
+        for (int j_ = 0; j_ < 4; ++j_) s_[12 + j_] = l_[9 + j_];                                    \
+        for (int j_ = 4; j_ < 11; ++j_) s_[12 + 3 + j_] = l_[9 + j_];                               \
       }                                                                                             \
-      if ((k) == 4) s_[9] = rt_;                                                                    \
     }                                                                                               \
   } while (0)
+#else
+#define NSTAMP(k)
+#endif
 #else
 #define NSTAMP(k)
 #endif
@@ -177,6 +216,13 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
       g.led_word_stride = 64;
     }
     NSTAMP(0);
+#if defined(SCG_NODES_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+    ScAcc acc_{};
+    g.dbg = &acc_;
+#define NACC(k) SCG_ACCP(&acc_, k)
+#else
+#define NACC(k)
+#endif
 
     // the step's observation row, whichever buffer(s) it goes to (chosen at the copy-out)
     ObsT* const orow = obs_t + lane * Op;
@@ -236,9 +282,11 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
     if (go)
       for (int i = w; i < NN; i += W) {
         const Num cst = sc_nodes_act<MAXD, !LED>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
+        NACC(12);
         cost_v[i * 64 + lane] = cst.v;
         cost_k[i * 64 + lane] = cst.k;
         for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
+        NACC(13);
       }
     NSTAMP(1);
     __syncthreads();
@@ -359,6 +407,7 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
       if (g.overflow) atomicOr(a.err, 1);
     }
     NSTAMP(4);
+#undef NACC
     // the next tile's stage rewrites the action tile, ret0 and, per wave, only the stock, size
     // and heap rows of its own nodes (whose stocks it copied back just above); the rows other
     // waves read (the observation tile) are next written after that tile's first barrier
@@ -427,6 +476,11 @@ int64_t sc_nodes_resident_blocks(int dev, int W, size_t lds) {
 #endif
 
 std::atomic<int> g_nodes_max_blocks{0};  // scg_sc_nodes_max_blocks (tests)
+#ifdef SCG_NODES_STAMPS
+constexpr size_t kNodesStaticLds = 8 * 20 * sizeof(unsigned long long);  // s_nodes_stamps
+#else
+constexpr size_t kNodesStaticLds = 0;
+#endif
 
 template <int MAXD, bool F64, bool LED>
 int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
@@ -437,7 +491,8 @@ int sc_launch_nodes_d(const ScArgs& a, int W, int E, hipStream_t s) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   if (lds > 64 * 1024 && !raised[dev].load(std::memory_order_acquire)) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sc_step_nodes_kernel<MAXD, F64, LED>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sc_nodes_lds_max())) != hipSuccess)
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(sc_nodes_lds_max() - kNodesStaticLds)) != hipSuccess)
       return fail(SCG_ERR_HIP, "node-parallel kernel: cannot raise its LDS limit");
     raised[dev].store(true, std::memory_order_release);
   }

@@ -148,6 +148,7 @@ __host__ __device__ inline Num sc_nodes_act(const ScCtx& c, ScEnv& g, const Node
   }
   if (!c.nodes[i].last_level) in.clear(c, i);
   sc_led_begin_node(c, g, i);
+  SCG_ACCP(g.dbg, 7);
   WordCache ltc{0, U4{0, 0, 0, 0}, false}, dmc{0, U4{0, 0, 0, 0}, false};
   return sc_node_act<MAXD, NodesInbox, true, kKindPaths>(c, g, ltc, dmc, i, act, t, in);
 }
@@ -170,6 +171,7 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
     const HeapEntry e{in.tk[(q0 + k) * in.stride], in.val[(q0 + k) * in.stride]};
     if (e.tk >= 0 && !py_heappush(lh, sz, c.H, e)) g.overflow = 1;
   }
+  SCG_ACCP(g.dbg, 0);
   if (receive) {
     double& st = sc_stock(c, g, i, p);
     st = st + sc_receive(lh, sz, t);
@@ -177,6 +179,7 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
     HeapEntry root = lh.get(0);
     while (sz > 0 && he_time(root.tk) == t) py_heappop_root(lh, sz, root);
   }
+  SCG_ACCP(g.dbg, 1);
   if (nd.n_supply > 0 && nd.supply_capacity[p] > 0) {
     const Num amount = np_mul(sc_action(act, nd.action_offset + a_i), pyint(nd.supply_capacity[p]));
     ++a_i;
@@ -186,6 +189,7 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
       ++lt_i;
     }
   }
+  SCG_ACCP(g.dbg, 2);
   const HeapView gh = sc_heap(c, g, i, p);
   sc_observe_bins(c, lh, sz, t, i, p, out, [&](int k, const HeapEntry& e) {  // copy back
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -198,6 +202,7 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
     gh.put(k, e);
   });
   sc_size(c, g, i, p) = sz;
+  SCG_ACCP(g.dbg, 3);
 }
 
 // The step of an env whose receive order sc_recv_scan could not prove, on the same staged

@@ -7,7 +7,10 @@ Runs sc-2perstage-v0 steps with kernel="nodes"; after each, reads the shader-clo
 lane 0 of every wave wrote (scg_sc_nodes.hip NSTAMP: 0 start, 5 heaps staged, 6 past the
 first barrier, 1 acted, 2 past the second, 3 heaps done, 7 past the third, 4 end) and prints per phase the median / p90 over waves, split by
 wave index in the block (wave w runs node w), and the spread of wave starts and ends
-(shader clocks, relative to the earliest start).
+(shader clocks, relative to the earliest start); then the clocks each wave spent in the
+sections of its act and heaps phases (sections_by_wave_p50, from the SCG_ACCP section stamps). With a
+persistent grid each wave's stamps are its last tile's: use --envs <= 64 x the resident
+blocks (32,768 on MI355X) for one tile per block.
 """
 import argparse
 import ctypes
@@ -43,7 +46,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(0)
     for _ in range(10):
         env.step(torch.rand((a.envs, env.n_actions), generator=gen, device=dev) * 2 - 1)
-    buf = np.zeros((min(waves, 1 << 14), 12), dtype=np.uint64)
+    buf = np.zeros((min(waves, 1 << 14), 28), dtype=np.uint64)
     for s in range(a.steps):
         act = torch.rand((a.envs, env.n_actions), generator=gen, device=dev) * 2 - 1
         torch.cuda.synchronize()
@@ -73,6 +76,22 @@ def main():
                               "block_end_pct": [float(np.percentile(be, q)) for q in (0, 25, 50, 75, 100)],
                               "block_dur_p50": float(np.median(be - bs)),
                               "clock_mhz": float(np.median(d[:, 7] / np.maximum(rt[:, 1] - rt[:, 0], 1e-3)))}
+        # section stamps (slot 12 + k = the clock at the end of section k, this launch's only
+        # when inside its phase): durations from the previous stamp of the same phase
+        secs = {"act": (6, [(7, "recv_clear"), (8, "stockpen_supply"), (9, "ship_split"), (10, "ship_dests"),
+                            (11, "ship_rest_or_retail"), (12, "holding"), (13, "cost_obs")], 1),
+                "heaps": (2, [(0, "inbox_push"), (1, "pops"), (2, "supply_push"), (3, "bins_copyback")], 3)}
+        sec_out = {}
+        for ph, (s0, lst, s1) in secs.items():
+            prev = st[:, s0].copy()
+            for k, nm in lst:
+                x = st[:, 12 + k]
+                ok = (x >= st[:, s0]) & (x <= st[:, s1])
+                dur = np.where(ok, x - prev, 0)
+                prev = np.where(ok, x, prev)
+                sec_out[f"{ph}.{nm}"] = [int(np.median(dur[wi == w])) for w in range(W)]
+            sec_out[f"{ph}.tail"] = [int(np.median((st[:, s1] - prev)[wi == w])) for w in range(W)]
+        out["sections_by_wave_p50"] = sec_out
         if a.dump:
             np.savez(f"{a.dump}_{s}.npz", stamps=st, W=W)
         print(json.dumps(out), flush=True)
