@@ -15,6 +15,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <ctime>
 #include <vector>
 
 #include "scg_beergame_kernels.h"
@@ -75,6 +76,15 @@ int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo
                 hipEvent_t ev1) {
   switch (L) {
 #define X(l) case l: return bg_launch_step<l>(grid, s, a, wk, ev0, ev1);
+    SCG_LEVEL_CASES(X)
+#undef X
+    default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
+  }
+}
+
+int launch_server(int L, hipStream_t s, const BgArgs& a, scg_bg_server_box* box, uint32_t last, uint32_t idle_ticks) {
+  switch (L) {
+#define X(l) case l: return bg_launch_server<l>(s, a, box, last, idle_ticks);
     SCG_LEVEL_CASES(X)
 #undef X
     default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
@@ -412,6 +422,106 @@ int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t*
   } else {
     st->week = w;
   }
+  if (done) *done = (wk.flags & 1) ? 1 : 0;
+  return SCG_OK;
+}
+
+// ---- step server (include/scgpu.h: scg_bg_server_step) ----------------------------------
+static int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000 + ts.tv_nsec;
+}
+
+static inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#endif
+}
+
+// Post request `cmd`: the request line's words (plan, and the action row when it travels
+// inline) written first, then its check, then the new request number; returns that number.
+static uint32_t server_post(scg_bg_server_box* b, int32_t cmd, uint32_t wpack, int32_t week, int32_t demand_fixed,
+                            int32_t n_inline, const int32_t* act) {
+  uint32_t w[16] = {0};
+  const uint32_t seq = __atomic_load_n(&b->req_seq, __ATOMIC_RELAXED) + 1;
+  w[0] = seq;
+  w[1] = static_cast<uint32_t>(cmd);
+  w[2] = wpack;
+  w[3] = static_cast<uint32_t>(week);
+  w[4] = static_cast<uint32_t>(demand_fixed);
+  w[5] = static_cast<uint32_t>(n_inline);
+  for (int l = 0; l < n_inline; ++l) w[8 + l] = static_cast<uint32_t>(act[l]);
+  w[7] = server_line_check(w);
+  uint32_t* line = reinterpret_cast<uint32_t*>(b);
+  for (int i = 1; i < 16; ++i) __atomic_store_n(&line[i], w[i], __ATOMIC_RELAXED);
+  __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);
+  return seq;
+}
+
+static int server_launch(const scg_bg_config* cfg, const scg_bg_state* st, scg_bg_server* sv) {
+  BgArgs a = make_args(cfg, st);
+  a.act = sv->action;
+  a.obs = sv->obs;
+  a.rew = sv->reward;
+  a.term_obs = nullptr;
+  const uint32_t last = __atomic_load_n(&sv->box_host->req_seq, __ATOMIC_ACQUIRE);
+  const uint32_t idle_ticks = static_cast<uint32_t>(sv->idle_us) * 100u;  // 100 MHz real-time clock
+  if (int rc = launch_server(cfg->levels, static_cast<hipStream_t>(sv->stream), a, sv->box_dev, last, idle_ticks))
+    return rc;
+  sv->running = 1;
+  sv->launches += 1;
+  sv->last_ns = mono_ns();
+  return SCG_OK;
+}
+
+int scg_bg_server_stop(scg_bg_server* sv) {
+  if (!sv || !sv->box_host) return fail(SCG_ERR_INVALID, "null server/mailbox");
+  if (!sv->running) return SCG_OK;
+  server_post(sv->box_host, 1, 0, 0, 0, 0, nullptr);
+  sv->running = 0;
+  if (hipStreamSynchronize(static_cast<hipStream_t>(sv->stream)) != hipSuccess)
+    return fail(SCG_ERR_HIP, "step server: hipStreamSynchronize failed");
+  return SCG_OK;
+}
+
+int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server* sv, int32_t* done) {
+  if (int rc = check_state(cfg, st)) return rc;
+  if (!sv || !sv->box_host || !sv->box_dev || !sv->action || !sv->obs || !sv->reward)
+    return fail(SCG_ERR_INVALID, "step server: mailbox, action, obs and reward are required");
+  if (st->n_envs > kServerBlock) return fail(SCG_ERR_INVALID, "the step server runs up to %d envs", kServerBlock);
+  if (cfg->variant != 1) return fail(SCG_ERR_INVALID, "the step server runs BeerGameEnv (variant 1)");
+  if (st->slab) return fail(SCG_ERR_INVALID, "the step server runs on separate state buffers (no slab)");
+  if (sv->idle_us < 100 || sv->idle_us > 10000000) return fail(SCG_ERR_INVALID, "idle_us outside 100..10^7");
+  if (int rc = check_step(cfg, st)) return rc;
+  const int32_t w = st->week + 1;
+  const WeekInfo wk = week_info(cfg, w, 0);
+  // a wave idle for more than half its time-out may be exiting: retire it before posting
+  if (sv->running && mono_ns() - sv->last_ns > static_cast<int64_t>(sv->idle_us) * 500)
+    if (int rc = scg_bg_server_stop(sv)) return rc;
+  scg_bg_server_box* b = sv->box_host;
+  for (int attempt = 0;; ++attempt) {
+    if (!sv->running)
+      if (int rc = server_launch(cfg, st, sv)) return rc;
+    const int32_t n_inline = (sv->action_host && st->n_envs == 1 && cfg->levels <= 8) ? cfg->levels : 0;
+    const uint32_t seq = server_post(b, 0, pack_week(wk), w, wk.demand_fixed, n_inline, sv->action_host);
+    const int64_t t0 = mono_ns();
+    bool served = true;
+    for (uint32_t spins = 0; __atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq; ++spins) {
+      cpu_relax();
+      if ((spins & 1023u) == 1023u && mono_ns() - t0 > 2000000000) {  // 2 s: the wave is gone or stuck
+        served = false;
+        break;
+      }
+    }
+    if (served) break;
+    const hipError_t q = hipStreamQuery(static_cast<hipStream_t>(sv->stream));
+    if (q == hipErrorNotReady || attempt > 0)
+      return fail(SCG_ERR_HIP, "step server: no answer from the wave for 2 s (week %d)", w);
+    sv->running = 0;  // it had exited (e.g. a host stall past its time-out): launch again
+  }
+  sv->last_ns = mono_ns();
+  st->week = w;  // no auto-reset on this path
   if (done) *done = (wk.flags & 1) ? 1 : 0;
   return SCG_OK;
 }

@@ -466,12 +466,13 @@ inline uint32_t pack_week_slab(const WeekInfo& wk) {
 // loads issue without waiting on the kernarg segment; the rest of the arguments arrive
 // through scalar loads that overlap those rows, and the Poisson inversion reads its
 // thresholds through the scalar cache, so it too runs while the rows are in flight.
-template <int L, int DM>
-__global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ inv_p, int32_t* __restrict__ bk_p,
-                                                         int32_t* __restrict__ op_p, const int32_t* __restrict__ act_p,
-                                                         int32_t* __restrict__ ring_p, uint32_t n32, uint32_t wpack,
-                                                         const BgArgs a, const WeekInfo wk) {
-  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+// (the week of env n < n32: the body of bg_step_kernel and of the step server below)
+// kActIn: the action row is act_in (already in registers), not read from act_p.
+template <int L, int DM, bool kActIn = false>
+__device__ __forceinline__ void bg_step_env(int64_t n, int32_t* __restrict__ inv_p, int32_t* __restrict__ bk_p,
+                                            int32_t* __restrict__ op_p, const int32_t* __restrict__ act_p,
+                                            int32_t* __restrict__ ring_p, uint32_t n32, uint32_t wpack,
+                                            const BgArgs& a, const WeekInfo& wk, const int32_t* act_in = nullptr) {
   const int32_t read_slot = static_cast<int32_t>(wpack & kWeekSlotMask) - 1;
   const int32_t write_slot = static_cast<int32_t>((wpack >> kWeekSlotBits) & kWeekSlotMask);
   const int32_t mode = static_cast<int32_t>((wpack >> 28) & 3u);
@@ -479,7 +480,6 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
   const bool autoreset = wpack & (2u << 30);
   const int64_t row = n * L;
   const int64_t stride = static_cast<int64_t>(n32) * L;
-  if (n >= static_cast<int64_t>(n32)) return;
 
   int32_t inv[L], bk[L], op[L], act[L], due[L], cur[L], iacc[L], bacc[L];
   zero_row<L>(due);
@@ -487,7 +487,12 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
   load_row<L>(inv_p + row, inv);
   load_row<L>(bk_p + row, bk);
   load_row<L>(op_p + row, op);
-  load_row<L>(act_p + row, act);
+  if constexpr (kActIn) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) act[l] = act_in[l];
+  } else {
+    load_row<L>(act_p + row, act);
+  }
   if (read_slot >= 0) load_row<L>(ring_p + read_slot * stride + row, due);
   if (mode == MODE_ADD) load_row<L>(ring_p + write_slot * stride + row, cur);
   // The remaining arguments are left to the compiler's scalar loads: they issue after
@@ -538,6 +543,74 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
   if (a.bk_acc) store_row<L>(a.bk_acc + row, bacc);    // :132
   if (a.ep_ret) a.ep_ret[n] = ret;
   note_overflow(a.err, ovf);
+}
+
+template <int L, int DM>
+__global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ inv_p, int32_t* __restrict__ bk_p,
+                                                         int32_t* __restrict__ op_p, const int32_t* __restrict__ act_p,
+                                                         int32_t* __restrict__ ring_p, uint32_t n32, uint32_t wpack,
+                                                         const BgArgs a, const WeekInfo wk) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (n >= static_cast<int64_t>(n32)) return;
+  bg_step_env<L, DM>(n, inv_p, bk_p, op_p, act_p, ring_p, n32, wpack, a, wk);
+}
+
+// ---- step server (scg_bg_server_step: the drop-in BeerGameEnv) ----------------------------
+// The request is one 64-byte line of the mailbox (scg_bg_server_box): 16 words, word 7 the
+// check over the others (include/scgpu.h), so a read that mixes two requests is detected.
+__host__ __device__ inline uint32_t server_line_check(const uint32_t (&w)[16]) {
+  uint32_t c = 0x9E3779B9u;
+  for (int i = 0; i < 16; ++i)
+    if (i != 7) c += w[i] * static_cast<uint32_t>(2 * i + 1);
+  return c;
+}
+
+// One wave, env n on lane n (a.n <= 64). Lanes 0-15 read the request line in one load
+// (system scope: past the caches, from host memory); on a new, consistent request the wave
+// runs the week body above with the posted plan — with env 0's action row from the line
+// itself when n_inline says it travelled there — then publishes the request number with a
+// system-scope release store after every lane's stores. It exits on cmd != 0, or when no
+// request has come for idle_ticks of the 100 MHz real-time clock, so it never outlives its
+// host process.
+constexpr int kServerBlock = 64;
+template <int L, int DM>
+__global__ __launch_bounds__(kServerBlock) void bg_server_kernel(const BgArgs a, scg_bg_server_box* box, uint32_t last,
+                                                                 uint32_t idle_ticks) {
+  const int64_t n = threadIdx.x;
+  const uint32_t* line = reinterpret_cast<const uint32_t*>(box);
+  uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint32_t v = __hip_atomic_load(line + (threadIdx.x & 15u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_readlane(v, i);
+    if (w[0] == last || w[7] != server_line_check(w)) {  // nothing new (or a torn read: again)
+      if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    last = w[0];
+    if (w[1] != 0) break;  // cmd: exit
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    WeekInfo wk{};
+    wk.week = static_cast<int32_t>(w[3]);
+    wk.demand_fixed = static_cast<int32_t>(w[4]);
+    if (n < a.n) {
+      if (L <= 8 && static_cast<int32_t>(w[5]) == L) {  // the action row came with the request
+        int32_t act_in[L];
+#pragma unroll
+        for (int l = 0; l < L; ++l) act_in[l] = static_cast<int32_t>(w[8 + (l < 8 ? l : 0)]);
+        bg_step_env<L, DM, true>(n, a.inv, a.bk, a.op, a.act, a.ring, static_cast<uint32_t>(a.n), w[2], a, wk, act_in);
+      } else {
+        bg_step_env<L, DM>(n, a.inv, a.bk, a.op, a.act, a.ring, static_cast<uint32_t>(a.n), w[2], a, wk);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every lane's stores before the answer
+    if (threadIdx.x == 0) __hip_atomic_store(&box->done_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    t0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (threadIdx.x == 0) __hip_atomic_store(&box->exit_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- slab step kernel -------------------------------------------------------------------
@@ -981,6 +1054,28 @@ int bg_launch_step(dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk
   }
 }
 
+template <int L>
+int bg_launch_server(hipStream_t s, const BgArgs& a, scg_bg_server_box* box, uint32_t last, uint32_t idle_ticks) {
+  switch (a.demand_mode) {
+    case SCG_DEMAND_FIXED:
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_FIXED>), dim3(1), dim3(kServerBlock), 0, s, a, box,
+                         last, idle_ticks);
+      break;
+    case SCG_DEMAND_TABLE:
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_TABLE>), dim3(1), dim3(kServerBlock), 0, s, a, box,
+                         last, idle_ticks);
+      break;
+    case SCG_DEMAND_UNIFORM:
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_UNIFORM>), dim3(1), dim3(kServerBlock), 0, s, a,
+                         box, last, idle_ticks);
+      break;
+    default:
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_POISSON>), dim3(1), dim3(kServerBlock), 0, s, a,
+                         box, last, idle_ticks);
+  }
+  return check_launch("bg_server_kernel");
+}
+
 template <int L, int DM>
 int bg_launch_slab_dm(dim3 grid, hipStream_t s, int32_t* slab, const int32_t* act, int32_t* out, uint32_t n32,
                       uint32_t wpack, uint32_t week, uint32_t episode, uint32_t k0, uint32_t k1, const BgSlabArgs& a,
@@ -1033,6 +1128,7 @@ int bg_launch_rollout(dim3 grid, hipStream_t s, const BgArgs& a, int32_t K, cons
   EXT template int bg_launch_reset<l>(dim3, hipStream_t, const BgArgs&);                                            \
   EXT template int bg_launch_step2<l>(dim3, hipStream_t, const BgArgs&, const WeekInfo&);                           \
   EXT template int bg_launch_step<l>(dim3, hipStream_t, const BgArgs&, const WeekInfo&, hipEvent_t, hipEvent_t);    \
+  EXT template int bg_launch_server<l>(hipStream_t, const BgArgs&, scg_bg_server_box*, uint32_t, uint32_t);         \
   EXT template int bg_launch_slab<l>(int, dim3, hipStream_t, int32_t*, const int32_t*, int32_t*, uint32_t, uint32_t, \
                                      uint32_t, uint32_t, uint32_t, uint32_t, const BgSlabArgs&, hipEvent_t,         \
                                      hipEvent_t);                                                                    \

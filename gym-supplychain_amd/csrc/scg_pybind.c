@@ -90,6 +90,21 @@ static PyObject* bg_step_timed(PyObject* self, PyObject* const* args, Py_ssize_t
   return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
 }
 
+/* bg_server_step(cfg, state, server): one week through the step server (scg_bg_server_step) */
+static PyObject* bg_server_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  void* p[3];
+  if (nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "bg_server_step expects 3 arguments");
+    return NULL;
+  }
+  for (int i = 0; i < 3; ++i)
+    if (as_ptr(args[i], &p[i])) return NULL;
+  int32_t done = 0;
+  const int rc = scg_bg_server_step((const scg_bg_config*)p[0], (scg_bg_state*)p[1], (scg_bg_server*)p[2], &done);
+  return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
+}
+
 /* sc_step(cfg, state, action, obs, reward, terminal_obs, flags, stream) */
 static PyObject* sc_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
   (void)self;
@@ -164,6 +179,7 @@ static PyObject* node_barrier(PyObject* self, PyObject* const* args, Py_ssize_t 
 static PyMethodDef methods[] = {
     {"bg_step", (PyCFunction)(void (*)(void))bg_step, METH_FASTCALL, "scg_bg_step"},
     {"bg_step_h", (PyCFunction)(void (*)(void))bg_step_h, METH_FASTCALL, "scg_bg_step with the fixed arguments behind a handle"},
+    {"bg_server_step", (PyCFunction)(void (*)(void))bg_server_step, METH_FASTCALL, "scg_bg_server_step"},
     {"bg_step_timed", (PyCFunction)(void (*)(void))bg_step_timed, METH_FASTCALL, "scg_bg_step_timed"},
     {"sc_step", (PyCFunction)(void (*)(void))sc_step, METH_FASTCALL, "scg_sc_step"},
     {"node_barrier", (PyCFunction)(void (*)(void))node_barrier, METH_FASTCALL, "host barrier of one node's ranks"},

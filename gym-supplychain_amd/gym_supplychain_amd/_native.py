@@ -16,7 +16,7 @@ import torch  # noqa: F401  (loads the HIP runtime libscgpu.so binds to)
 
 LIB_NAME = "libscgpu.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 SCG_OK = 0
 SCG_ERR_INVALID = 1
@@ -101,6 +101,22 @@ class BgState(ctypes.Structure):
     ]
 
 
+class BgServerBox(ctypes.Structure):
+    """scg_bg_server_box (include/scgpu.h): the step server's mailbox, in host-mapped memory."""
+    _fields_ = [("req_seq", ctypes.c_uint32), ("cmd", ctypes.c_int32), ("wpack", ctypes.c_uint32),
+                ("week", ctypes.c_int32), ("demand_fixed", ctypes.c_int32), ("n_inline", ctypes.c_int32),
+                ("pad0", ctypes.c_int32), ("check", ctypes.c_uint32), ("action", ctypes.c_int32 * 8),
+                ("done_seq", ctypes.c_uint32), ("exit_seq", ctypes.c_uint32), ("pad1", ctypes.c_int32 * 14)]
+
+
+class BgServer(ctypes.Structure):
+    """scg_bg_server (include/scgpu.h): the step server's launch arguments and host bookkeeping."""
+    _fields_ = [("box_host", ctypes.c_void_p), ("box_dev", ctypes.c_void_p), ("action", ctypes.c_void_p),
+                ("action_host", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p),
+                ("stream", ctypes.c_void_p), ("idle_us", ctypes.c_int32), ("running", ctypes.c_int32),
+                ("last_ns", ctypes.c_int64), ("launches", ctypes.c_int64)]
+
+
 # scg_bg_slab_field: word offsets of a BeerGame state slab (scg_bg_slab_layout)
 (SLAB_ERROR, SLAB_INVENTORY, SLAB_BACKLOG, SLAB_ORDERS, SLAB_INV_COSTS, SLAB_BACKLOG_COSTS, SLAB_TERMINAL_OBS,
  SLAB_RING, SLAB_EPISODE_RETURN, SLAB_FINAL_RETURN, SLAB_HISTORY, SLAB_TOTAL, SLAB_FIELDS) = range(13)
@@ -182,6 +198,9 @@ SIGNATURES = {
     "scg_bg_step_timed": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          _i32p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "scg_bg_server_step": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState),
+                                          ctypes.POINTER(BgServer), _i32p]),
+    "scg_bg_server_stop": (ctypes.c_int, [ctypes.POINTER(BgServer)]),
     "scg_bg_rollout": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p]),

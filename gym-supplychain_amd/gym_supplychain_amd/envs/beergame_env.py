@@ -12,8 +12,10 @@ Differences from the reference, all documented in DESIGN.md:
   * BeerGameVecEnv adds per-env demand (a device table, or Poisson draws made on device
     with Philox4x32-10) and auto-reset; the reference has one fixed demand list (F2).
 """
+import atexit
 import ctypes
 import numbers
+import os
 import weakref
 
 import numpy as np
@@ -529,6 +531,65 @@ class BeerGameVecEnv:
         pass
 
 
+_SERVERS = weakref.WeakSet()
+
+
+@atexit.register
+def _stop_servers():  # no step-server wave outlives the interpreter (nor its mailbox)
+    for sv in list(_SERVERS):
+        sv.close()
+
+
+class _StepServer:
+    """The drop-in env's step server (include/scgpu.h scg_bg_server_step): one wave on a
+    non-blocking stream of its own polls a mailbox in host-mapped memory and runs each posted
+    week on the vec env's state. It exits when stopped, or by itself after IDLE_US without a
+    request; step() launches it again when needed. The mailbox is this object's own, freed
+    only after the wave has been stopped (the wave reads nothing else while it waits)."""
+
+    IDLE_US = 20000
+
+    def __init__(self, vec, act_dev, act_host, obs_dev, rew_dev):
+        hip = nat.hip_runtime()
+        hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+        stream = ctypes.c_void_p()
+        with torch.cuda.device(vec.device):
+            if hip.hipStreamCreateWithFlags(ctypes.byref(stream), 1) != 0:  # hipStreamNonBlocking
+                raise RuntimeError("hipStreamCreateWithFlags failed")
+        self._hip, self._vec, self._device = hip, vec, vec.device
+        self._box = box = nat.MappedBuffer(ctypes.sizeof(nat.BgServerBox))
+        self.sv = nat.BgServer(box.host, box.dev, act_dev, act_host, obs_dev, rew_dev, stream.value, self.IDLE_US, 0, 0,
+                               0)
+        self._args = (vec._cfg_addr, vec._st_addr, ctypes.addressof(self.sv))
+        self._fast = nat.fast.bg_server_step
+        self._closed = False
+        _SERVERS.add(self)
+
+    def step(self):
+        return self._fast(*self._args)
+
+    def stop(self):
+        if not self._closed:
+            with torch.cuda.device(self._device):
+                nat.check(nat.lib.scg_bg_server_stop(ctypes.byref(self.sv)))
+
+    def close(self):
+        if self._closed:
+            return
+        self.stop()  # raises if the wave cannot be stopped: then the mailbox stays allocated
+        self._closed = True
+        self._hip.hipStreamDestroy(ctypes.c_void_p(self.sv.stream))
+        self._box = None
+        _SERVERS.discard(self)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass
+
+
 class BeerGameEnv(spaces.Env):
     """Drop-in for gym_supplychain.envs.BeerGameEnv (beergame_env.py:6-181), one env.
 
@@ -562,8 +623,7 @@ class BeerGameEnv(spaces.Env):
         self.current_state = None
         # one host-mapped block for the step's inputs and outputs: the overflow word (the
         # kernel's plain store of 1, cleared by reset), the action row, and the observation
-        # row + reward; a step is one launch and one stream synchronisation, no copies
-        # (profiles/r05*_facade_latency.log)
+        # row + reward (profiles/r05*_facade_latency.log)
         ra = (4 * L + 15) // 16 * 16
         self._io = io = nat.MappedBuffer(16 + ra + 4 * (L + 1))
         self._err_np = io.view(np.int32, 0, 1)
@@ -573,8 +633,14 @@ class BeerGameEnv(spaces.Env):
         vec = self._vec
         vec._st.error_flags = io.dev
         vec._err = torch.from_numpy(self._err_np)  # check_errors() reads the mapped word
-        self._step_args = nat.BgStepArgs(vec._cfg_addr, vec._st_addr, io.dev + 16 + ra, io.dev + 16 + ra + 4 * L,
-                                         vec._term_ptr, 0)
+        obs_dev, rew_dev = io.dev + 16 + ra, io.dev + 16 + ra + 4 * L
+        # The week runs on a resident wave that polls the mailbox (scg_bg_server_step): no
+        # launch and no stream synchronisation per step. SCG_BG_SERVER=0: one launch of the
+        # step kernel plus one synchronisation per step instead.
+        self._server = None
+        if os.environ.get("SCG_BG_SERVER", "1") != "0":
+            self._server = _StepServer(self._vec, self._act_dev, io.host + 16, obs_dev, rew_dev)
+        self._step_args = nat.BgStepArgs(vec._cfg_addr, vec._st_addr, obs_dev, rew_dev, vec._term_ptr, 0)
         self._handle = ctypes.addressof(self._step_args)
         self._fast_step_h = nat.fast.bg_step_h
         self._sync = nat.stream_synchronize_fn()
@@ -582,10 +648,12 @@ class BeerGameEnv(spaces.Env):
         self.week = None
 
     def reset(self):
+        if self._server is not None:
+            self._server.stop()  # the reset kernel rewrites the state the wave steps
         obs = self._vec.reset()
         self.week = 0
         self._last_act = None
-        self.current_state = obs[0].cpu().numpy().astype(np.int64)
+        self.current_state = obs[0].cpu().numpy().astype(np.int64)  # waits for the reset kernel
         return self.current_state
 
     def step(self, action):
@@ -594,14 +662,22 @@ class BeerGameEnv(spaces.Env):
         a = np.asarray(action)
         if a.dtype.kind == "f":
             a = np.trunc(a)
-        self._act_np[:] = np.broadcast_to(a, (self.levels,))
-        stream = self._vec._raw_stream(self._vec._dev_index)
-        r = self._fast_step_h(self._handle, self._act_dev, stream)
-        if r > 1:
-            nat.check(r >> 1)
-        rc = self._sync(stream)
-        if rc:
-            raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
+        if a.shape == self._act_np.shape:
+            self._act_np[:] = a
+        else:
+            self._act_np[:] = np.broadcast_to(a, (self.levels,))
+        if self._server is not None:
+            r = self._server.step()  # returns once the wave has written obs and reward
+            if r > 1:
+                nat.check(r >> 1)
+        else:
+            stream = self._vec._raw_stream(self._vec._dev_index)
+            r = self._fast_step_h(self._handle, self._act_dev, stream)
+            if r > 1:
+                nat.check(r >> 1)
+            rc = self._sync(stream)
+            if rc:
+                raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
         if int(self._err_np[0]):  # the reference's int64 values no longer fit the int32 state
             raise OverflowError("a BeerGame value left int32 range; the GPU state no longer matches the reference")
         L = self.levels
@@ -675,7 +751,13 @@ class BeerGameEnv(spaces.Env):
         print('Backlog costs:\t', self.backlog_costs)
 
     def close(self):
-        pass
+        if self._server is not None:
+            self._server.close()
+
+    def __del__(self):
+        server = getattr(self, "_server", None)
+        if server is not None:
+            server.close()
 
     def _observation(self):
         return self.inventory - self.backlog

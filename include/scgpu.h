@@ -36,8 +36,10 @@ extern "C" {
 #endif
 
 /* 5 (round 4): scg_sc_state.inbox_tk is uint8 [inbox_size][N] (byte-packed entries);
- *   shipment delays up to SCG_BG_MAX_DELAY = 4096; full_table of any row count. */
-#define SCG_ABI_VERSION 5
+ *   shipment delays up to SCG_BG_MAX_DELAY = 4096; full_table of any row count.
+ * 6 (round 5): the BeerGame step server (scg_bg_server_box, scg_bg_server, scg_bg_server_step,
+ *   scg_bg_server_stop) and the testing hook scg_sc_nodes_max_blocks. */
+#define SCG_ABI_VERSION 6
 
 #if defined(__GNUC__)
 #define SCG_API __attribute__((visibility("default")))
@@ -237,6 +239,60 @@ SCG_API int scg_bg_step(const scg_bg_config* cfg, scg_bg_state* st, const int32_
 SCG_API int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t* action,
                               int32_t* obs, int32_t* reward, int32_t* terminal_obs, uint32_t flags,
                               int32_t* done, void* start_event, void* stop_event, void* stream);
+
+/*
+ * Step server for a few envs stepped one week per host call (the drop-in BeerGameEnv:
+ * beergame_env.py:66-138 is one Python call per week). A launch plus a stream
+ * synchronisation per week costs more than the reference's whole step, so instead one wave
+ * stays resident: it polls a mailbox in host-mapped memory, runs the week body of
+ * bg_step_kernel (the same code, the same state buffers) when scg_bg_server_step posts a
+ * week's plan, and writes obs / reward to the caller's buffers (host-mapped, so the host reads
+ * them at once). Up to 64 envs, variant 1, separate state buffers (no slab), no auto-reset.
+ *
+ * The wave exits on scg_bg_server_stop, or by itself after idle_us without a request, so it
+ * never outlives its process; scg_bg_server_step (re)launches it when it is not running or
+ * may have timed out (idle for more than idle_us / 2 on the host's clock). Work the caller
+ * launches on the state (reset, other steps) must be complete before scg_bg_server_step and
+ * must not start before scg_bg_server_stop returns; the mailbox must outlive the wave.
+ */
+typedef struct scg_bg_server_box {  /* host-mapped (hipHostMalloc mapped + coherent), 128 B */
+  /* the request: one 64-byte line, which the wave reads in one load */
+  uint32_t req_seq;      /* request number (a new number is a new request)                   */
+  int32_t cmd;           /* 0 step, 1 exit                                                  */
+  uint32_t wpack;        /* the week's plan, as bg_step_kernel's packed word                */
+  int32_t week;          /* the week being stepped (1..max_weeks)                           */
+  int32_t demand_fixed;  /* customer_demand[week - 1] for SCG_DEMAND_FIXED                  */
+  int32_t n_inline;      /* L when env 0's action row travels in action[] (one env, L <= 8) */
+  int32_t pad0;
+  uint32_t check;        /* 0x9E3779B9 + sum over the line's words i != 7 of word_i * (2i + 1),
+                            mod 2^32: a read of the line that mixes two requests is read again */
+  int32_t action[8];
+  /* the answer, on its own line */
+  uint32_t done_seq;     /* last request served                                             */
+  uint32_t exit_seq;     /* last request seen when the wave exited                          */
+  int32_t pad1[14];
+} scg_bg_server_box;
+
+typedef struct scg_bg_server {
+  scg_bg_server_box* box_host;  /* the mailbox's host address                             */
+  scg_bg_server_box* box_dev;   /* its device address (hipHostGetDevicePointer)           */
+  const int32_t* action;        /* DEVICE-visible int32 [N][L], read each request         */
+  const int32_t* action_host;   /* its host address, or NULL: with one env of L <= 8, the
+                                   row is copied into the request line (no second read)  */
+  int32_t* obs;                 /* DEVICE-visible int32 [N][L]                            */
+  int32_t* reward;              /* DEVICE-visible int32 [N]                               */
+  void* stream;                 /* the wave's stream: a non-blocking one of the caller's  */
+  int32_t idle_us;              /* the wave exits after this long without a request       */
+  int32_t running;              /* out: the wave may be running                           */
+  int64_t last_ns;              /* out: host monotonic time of the last request served    */
+  int64_t launches;             /* out: waves launched so far                             */
+} scg_bg_server;
+
+/* step(action) for the st->n_envs <= 64 envs through the server wave; *done as scg_bg_step. */
+SCG_API int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server* sv, int32_t* done);
+
+/* Ask the server wave to exit and wait for it (a no-op when it is not running). */
+SCG_API int scg_bg_server_stop(scg_bg_server* sv);
 
 /*
  * K consecutive steps in one launch per <= SCG_BG_ROLLOUT_MAX weeks, state held in

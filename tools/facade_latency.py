@@ -5,10 +5,12 @@ of the reference step() on one host core.
     python tools/facade_latency.py [--bg-episodes 100] [--sc-episodes 3]
 
 * BeerGameEnv.step (beergame_env.py:66-138; reference ~12.8 us per step on one core,
-  BASELINE.md §4): the facade writes the action into host-mapped memory, launches the step
-  kernel, synchronises the stream and reads observation, reward and the overflow word from
-  host-mapped memory — `copies` times the previous design (pinned H2D copy, launch, two D2H
-  copies, synchronise) on the same box for comparison.
+  BASELINE.md §4): the facade writes the action into host-mapped memory and posts the week
+  to its step server (a resident wave polling a host-mapped mailbox, scg_bg_server_step),
+  which writes observation, reward and the overflow word to host-mapped memory; beside it the
+  launch path (SCG_BG_SERVER=0: one step-kernel launch and one stream synchronisation per
+  call) and the round-4 design (pinned H2D copy, launch, two D2H copies, synchronise), on the
+  same box. The server's wave launches are counted (one per episode: reset() stops it).
 * SupplyChain2perStageEnv.step (supplychain_env.py:703-748; reference ~136 us per step):
   the same host-mapped path, host RandomState episode draws (the reference's), float64 obs.
 * cpu: oracle.beergame.BeerGameOracle.step and oracle.supplychain.SupplyChainOracle.step
@@ -48,14 +50,19 @@ def _time_episodes(env, actions, episodes, horizon):
     return ts
 
 
-def beergame(episodes):
+def beergame(episodes, server=True):
     import numpy as np
+    os.environ["SCG_BG_SERVER"] = "1" if server else "0"
     import gym_supplychain_amd as gsa
     env = gsa.make("beergame-v0")
     rng = np.random.RandomState(0)
     acts = [rng.randint(0, 9, size=4) for _ in range(35 * 8)]
     _time_episodes(env, acts, 2, 35)  # warm-up
-    return _stats(_time_episodes(env, acts, episodes, 35))
+    st = _stats(_time_episodes(env, acts, episodes, 35))
+    if server:
+        st["server_wave_launches"] = int(env._server.sv.launches)
+    env.close()
+    return st
 
 
 class _CopyingBeerGame:
@@ -156,7 +163,9 @@ def main():
     def emit(what, ref_us, st, **kw):
         print(json.dumps({"measure": what, "device": dev, "reference_us_per_step": ref_us, **st, **kw}), flush=True)
 
-    emit("BeerGameEnv.step (host-mapped io, one launch + stream sync)", 12.8, beergame(a.bg_episodes))
+    emit("BeerGameEnv.step (step server: resident wave, host-mapped mailbox and io)", 12.8, beergame(a.bg_episodes))
+    emit("BeerGameEnv.step, launch path (SCG_BG_SERVER=0: host-mapped io, one launch + stream sync)", 12.8,
+         beergame(a.bg_episodes, server=False))
     emit("BeerGameEnv.step, round-4 design (H2D copy, launch, 2 D2H copies, sync)", 12.8, beergame_copies(a.bg_episodes))
     st, kernel = supplychain(a.sc_episodes)
     emit("SupplyChain2perStageEnv.step (host-mapped io, one launch + stream sync)", 136.0, st, kernel=kernel)
