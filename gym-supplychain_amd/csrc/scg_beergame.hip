@@ -500,25 +500,38 @@ int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server
   if (sv->running && mono_ns() - sv->last_ns > static_cast<int64_t>(sv->idle_us) * 500)
     if (int rc = scg_bg_server_stop(sv)) return rc;
   scg_bg_server_box* b = sv->box_host;
-  for (int attempt = 0;; ++attempt) {
+  // Waiting for the answer, every 2 s: a wave that has exited without serving the request
+  // (its stream is idle: e.g. a host stall past its time-out) is launched again and the week
+  // posted again, once; a wave still queued or running is waited for, up to 60 s in all (a
+  // busy GPU may start it late).
+  const int64_t start = mono_ns();
+  for (int relaunched = 0;;) {
     if (!sv->running)
       if (int rc = server_launch(cfg, st, sv)) return rc;
     const int32_t n_inline = (sv->action_host && st->n_envs == 1 && cfg->levels <= 8) ? cfg->levels : 0;
     const uint32_t seq = server_post(b, 0, pack_week(wk), w, wk.demand_fixed, n_inline, sv->action_host);
-    const int64_t t0 = mono_ns();
-    bool served = true;
-    for (uint32_t spins = 0; __atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq; ++spins) {
-      cpu_relax();
-      if ((spins & 1023u) == 1023u && mono_ns() - t0 > 2000000000) {  // 2 s: the wave is gone or stuck
-        served = false;
+    bool served = false, gone = false;
+    int64_t check = mono_ns() + 2000000000;
+    for (uint32_t spins = 0;; ++spins) {
+      if (__atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) == seq) {
+        served = true;
         break;
       }
+      cpu_relax();
+      if ((spins & 1023u) != 1023u) continue;
+      const int64_t now = mono_ns();
+      if (now < check) continue;
+      check = now + 2000000000;
+      if (hipStreamQuery(static_cast<hipStream_t>(sv->stream)) == hipSuccess &&
+          __atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq) {
+        gone = true;
+        break;
+      }
+      if (now - start > 60000000000LL) return fail(SCG_ERR_HIP, "step server: no answer for 60 s (week %d)", w);
     }
     if (served) break;
-    const hipError_t q = hipStreamQuery(static_cast<hipStream_t>(sv->stream));
-    if (q == hipErrorNotReady || attempt > 0)
-      return fail(SCG_ERR_HIP, "step server: no answer from the wave for 2 s (week %d)", w);
-    sv->running = 0;  // it had exited (e.g. a host stall past its time-out): launch again
+    if (gone && relaunched++ > 0) return fail(SCG_ERR_HIP, "step server: the wave exits without answering (week %d)", w);
+    sv->running = 0;
   }
   sv->last_ns = mono_ns();
   st->week = w;  // no auto-reset on this path
