@@ -659,7 +659,7 @@ class SupplyChainEnv(spaces.Env):
                  demand_config_by_product=False, demand_range=(10, 20), demand_std=None, demand_sen_peaks=None,
                  avg_demand_range=None, processing_ratio=3, stochastic_leadtimes=False, avg_leadtime=2,
                  max_leadtime=2, total_time_steps=360, seed=None, build_info=False, demand_perturb_norm=False,
-                 device=None, host_rng=True):
+                 device=None, host_rng=True, kernel=None):
         dkw = dict(demand_config_by_product=demand_config_by_product, demand_range=demand_range,
                    demand_std=demand_std, demand_sen_peaks=demand_sen_peaks, avg_demand_range=avg_demand_range,
                    demand_perturb_norm=demand_perturb_norm)
@@ -682,8 +682,21 @@ class SupplyChainEnv(spaces.Env):
             vec_kw["demand_table"] = torch.zeros((1, T + 1, R, P), dtype=torch.int32, device=dev)
             if spec.stochastic_leadtimes:
                 vec_kw["leadtime_table"] = torch.ones((1, T, spec.n_leadtimes), dtype=torch.int32, device=dev)
-        self._vec = SupplyChainVecEnv(1, spec=spec, seed=seed, device=device, auto_reset=False,
-                                      obs_dtype=torch.float64, **vec_kw)
+        # One env is a latency path, not an occupancy one: the node-parallel kernel (every node
+        # of the env on its own wave) whenever the chain qualifies, which the "auto" choice, made
+        # for batches, skips when two blocks of it would not share a CU (sc-2perstage, float64
+        # observations: 26.9 against 58.3 us per step() for the lane kernel,
+        # profiles/r05zz_sc_facade_kernels.log); otherwise the auto choice.
+        self._vec = None
+        if kernel is None:
+            try:
+                self._vec = SupplyChainVecEnv(1, spec=spec, seed=seed, device=device, auto_reset=False,
+                                              obs_dtype=torch.float64, kernel="nodes", **vec_kw)
+            except ValueError:  # the chain does not qualify (scg_sc_prepare)
+                self._vec = None
+        if self._vec is None:
+            self._vec = SupplyChainVecEnv(1, spec=spec, seed=seed, device=device, auto_reset=False,
+                                          obs_dtype=torch.float64, kernel=kernel or "auto", **vec_kw)
         self.num_products = spec.P
         self.total_time_steps = spec.total_time_steps
         self.stochastic_leadtimes = spec.stochastic_leadtimes
