@@ -147,6 +147,59 @@ def test_step_rejects_shards_beyond_int32_before_any_launch():
     assert rc == nat.SCG_ERR_INVALID and "n_envs" in nat.last_error()
 
 
+def test_step_server_validates_before_any_launch():
+    """scg_bg_server_step / scg_bg_server_stop: every argument the resident wave depends on is
+    checked on the host before anything is launched (more than 64 envs, BeerGameEnv2, the slab
+    layout, a missing mailbox or buffer, an idle time-out out of range, a step before reset or
+    past the horizon); stopping a server that never ran is a no-op."""
+    from gym_supplychain_amd import _native as nat
+    T = 35
+    c = nat.BgConfig()
+    c.levels, c.max_weeks = 4, T
+    d = (ctypes.c_int32 * (T + 1))(*([2] * (T + 1)))
+    dem = (ctypes.c_int32 * T)(*([8] * T))
+    plan = (ctypes.c_int32 * (T + 1))()
+    c.shipment_delays = ctypes.cast(d, ctypes.c_void_p)
+    c.customer_demand = ctypes.cast(dem, ctypes.c_void_p)
+    c.plan = ctypes.cast(plan, ctypes.c_void_p)
+    assert nat.lib.scg_bg_prepare(ctypes.byref(c)) == 0
+    fake = 0x1000  # never dereferenced: every call below fails validation first
+    st = nat.BgState()
+    st.n_envs, st.env_offset, st.week = 1, 0, 0
+    for f in ("inventory", "backlog", "orders_placed", "shipments"):
+        setattr(st, f, fake)
+    box = nat.BgServerBox()
+    sv = nat.BgServer(ctypes.addressof(box), fake, fake, None, fake, fake, None, 20000, 0, 0, 0)
+    done = ctypes.c_int32(0)
+
+    def step(expect, text):
+        rc = nat.lib.scg_bg_server_step(ctypes.byref(c), ctypes.byref(st), ctypes.byref(sv), ctypes.byref(done))
+        assert rc == expect and text in nat.last_error(), (rc, nat.last_error())
+
+    st.n_envs = 65
+    step(nat.SCG_ERR_INVALID, "64")
+    st.n_envs = 1
+    sv.obs = None
+    step(nat.SCG_ERR_INVALID, "required")
+    sv.obs = fake
+    sv.idle_us = 10
+    step(nat.SCG_ERR_INVALID, "idle_us")
+    sv.idle_us = 20000
+    st.slab = fake
+    step(nat.SCG_ERR_INVALID, "slab")
+    st.slab = None
+    st.week = -1
+    step(nat.SCG_ERR_NOT_RESET, "reset")
+    st.week = T
+    step(nat.SCG_ERR_PAST_HORIZON, "terminal")
+    c.variant = 2
+    st.week = 0
+    step(nat.SCG_ERR_INVALID, "variant 1")
+    assert sv.running == 0 and sv.launches == 0 and box.req_seq == 0  # nothing was posted or launched
+    assert nat.lib.scg_bg_server_stop(ctypes.byref(sv)) == 0
+    assert nat.lib.scg_bg_server_stop(None) == nat.SCG_ERR_INVALID
+
+
 def test_uniform_ints_rejects_env_ids_and_sizes_before_any_launch():
     """scg_uniform_ints: the Philox env counter is 32-bit and the per-env word count int32, so
     ids past 2^32 and rows*width past INT32_MAX are rejected before any HIP call."""
