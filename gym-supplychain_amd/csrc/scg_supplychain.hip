@@ -735,7 +735,8 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
   for (int i = 0; i < NN; ++i)
     for (int p = 0; p < P; ++p)
       for (int j = 0; j < nodes[i].n_init[p]; ++j) rel_max = std::max(rel_max, nodes[i].init_time[p][j]);
-  const bool staged_ok = rel_max <= kStagedMaxRel;
+  // ... and its ship capacities as overflow bits (ShipLeftBits): (P - 1) * MAXD <= 64
+  const bool staged_ok = rel_max <= kStagedMaxRel && (!SCG_STAGED_SHIP_BITS || (P - 1) * sc_maxd_bucket(maxd) <= 64);
   if (want == SCG_SC_KERNEL_AUTO && staged_ok && sc_lds_bytes(cfg) > kScLdsMax && sc_staged_lds_bytes(cfg) <= kScLdsMax) {
     std::vector<scg_sc_node> probe(nodes, nodes + NN);
     if (sc_inbox_layout(cfg, probe.data()) >= 0) want = SCG_SC_KERNEL_STAGED;
@@ -762,8 +763,11 @@ int scg_sc_prepare(scg_sc_config* cfg, scg_sc_node* nodes) {
       return fail(SCG_ERR_INVALID, "the staged kernel needs every shipment to go to a later node, once per list");
     if (sc_staged_lds_bytes(cfg) > kScLdsMax)
       return fail(SCG_ERR_INVALID, "one node's heaps (%d products x %d slots) exceed the staged kernel's LDS", P, H);
-    if (!staged_ok)
+    if (rel_max > kStagedMaxRel)
       return fail(SCG_ERR_INVALID, "the staged kernel holds lead times up to %d (this chain: %d)", kStagedMaxRel, rel_max);
+    if (!staged_ok)
+      return fail(SCG_ERR_INVALID, "the staged kernel takes (products - 1) x destinations <= 64 (this chain: %d x %d)",
+                  P - 1, sc_maxd_bucket(maxd));
     cfg->inbox_size = entries;
     cfg->kernel = SCG_SC_KERNEL_STAGED;
     cfg->layout = SCG_SC_LAYOUT_ENV_FASTEST;

@@ -354,6 +354,7 @@ struct DirectPush {
   static constexpr bool kLdsSplit = false;  // see sc_split_scratch
   static constexpr bool kVecActions = false;  // see sc_ship_vals
   static constexpr bool kClearInAct = false;  // see StagedInbox::noship
+  static constexpr bool kShipBits = false;    // see ShipLeftBits
   __host__ __device__ Num scratch_get(int) const { return pyint(0); }
   __host__ __device__ void noship(const ScCtx&, int, int, int) const {}
   __host__ __device__ void noship_all(const ScCtx&, int, int) const {}
@@ -412,6 +413,50 @@ struct NumVec {
     for (int j = 0; j < (MAXD + 7) / 8; ++j)
       kw[j] = (j == (i >> 3)) ? ((kw[j] & ~(15u << sh)) | (static_cast<uint32_t>(x.k) << sh)) : kw[j];
   }
+};
+
+// available_ship_capacities (:265), shared by a node's products: destination i's ship
+// capacity, cut only when a product's shipment overflows it (:312-328), to the capacity minus
+// what left (the shipment re-set to the capacity, times the processing ratio at a factory).
+// Every value it takes is a Python int (an int capacity, minus an int times an int), so the
+// kind never rounds anything to float32.
+//   ShipLeftVec: the values themselves, one register pair per destination.
+//   ShipLeftBits: one bit per (earlier product, destination) saying the capacity overflowed;
+//     the value is rebuilt from the capacity by the same int operations in product order (a
+//     destination is visited once per product). For the staged kernel, whose MAXD = 16
+//     values were 48 of its 249 VGPRs; needs (P - 1) * MAXD <= 64 (scg_sc_prepare).
+template <int MAXD>
+struct ShipLeftVec {
+  NumVec<MAXD> v;
+  __host__ __device__ __forceinline__ void init(ScNode& nd, int D) {
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) v.set(i, pyint(i < D ? nd.ship_capacity[i] : 0));
+  }
+  __host__ __device__ __forceinline__ Num get(ScNode&, bool, int i, int) const { return v.get_dyn(i); }
+  __host__ __device__ __forceinline__ void overflowed(int i, int, Num left) { v.set_dyn(i, left); }
+  __host__ __device__ __forceinline__ bool any_f32() const {
+    bool f = false;
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j) f |= v.get(j).k == NK_F32;
+    return f;
+  }
+};
+
+template <int MAXD>
+struct ShipLeftBits {
+  uint64_t ovf;
+  __host__ __device__ __forceinline__ void init(ScNode&, int) { ovf = 0; }
+  __host__ __device__ __forceinline__ Num get(ScNode& nd, bool factory, int i, int p) const {
+    double c = static_cast<double>(nd.ship_capacity[i]);
+    for (int q = 0; q < p; ++q)
+      if ((ovf >> (q * MAXD + i)) & 1u) c = c - (factory ? c * static_cast<double>(nd.processing_ratio[q]) : c);
+    return pyint(c);
+  }
+  // (the last product's overflows are never read back, and need no bit)
+  __host__ __device__ __forceinline__ void overflowed(int i, int p, Num) {
+    if ((p + 1) * MAXD <= 64) ovf |= uint64_t(1) << (p * MAXD + i);
+  }
+  __host__ __device__ __forceinline__ bool any_f32() const { return false; }
 };
 
 // SC_Action.apply for SHIP (:58-96): the cut [0, limit] split at the destinations'
@@ -631,9 +676,9 @@ __host__ __device__ __forceinline__ Num sc_node_act(const ScCtx& c, ScEnv& e, Wo
   if (!nd.last_level) {
     // SHIP (:262-375)
     const int D = nd.n_dests;
-    NumVec<MAXD> ship_left;  // available_ship_capacities, shared by the products (:265)
-#pragma unroll
-    for (int i = 0; i < MAXD; ++i) ship_left.set(i, pyint(i < D ? nd.ship_capacity[i] : 0));
+    // available_ship_capacities, shared by the products (:265)
+    typename std::conditional<Push::kShipBits, ShipLeftBits<MAXD>, ShipLeftVec<MAXD>>::type ship_left;
+    ship_left.init(nd, D);
     Num proc_left = pyint(nd.processing_capacity);
     const int lt_base = lt_i;
     const bool factory = nd.processing_capacity > 0;
@@ -652,8 +697,7 @@ __host__ __device__ __forceinline__ Num sc_node_act(const ScCtx& c, ScEnv& e, Wo
         // either (the stock is the limit, or nothing is cut) every promoted kind is float64 or
         // a Python / int64 scalar, and the whole wave runs the plain double instantiation.
         bool f32_left = proc_left.k == NK_F32;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) f32_left |= ship_left.get(j).k == NK_F32;
+        f32_left |= ship_left.any_f32();
         const bool no32 = kKindPaths && wave_all(!f32_left && (limit.k != NK_INT || !np_lt(pyint(0), limit)));
         auto ship_product = [&](auto no32_tag) __attribute__((always_inline)) {
           constexpr bool kNo32 = decltype(no32_tag)::value;
@@ -696,12 +740,12 @@ __host__ __device__ __forceinline__ Num sc_node_act(const ScCtx& c, ScEnv& e, Wo
               }
               snt = np_div_k<kNo32>(o, pyint(nd.processing_ratio[p]));
             }
-            const Num cap = ship_left.get_dyn(i);
+            const Num cap = ship_left.get(nd, factory, i, p);
             if (np_lt_k<kNo32>(pyint(0), snt) && np_lt_k<kNo32>(cap, snt)) {
               over_ship = np_add_k<kNo32>(over_ship, np_sub_k<kNo32>(snt, cap));
               snt = cap;
               o = factory ? np_mul_k<kNo32>(snt, pyint(nd.processing_ratio[p])) : snt;
-              ship_left.set_dyn(i, np_sub_k<kNo32>(cap, o));  // only on overflow, by the new amount
+              ship_left.overflowed(i, p, np_sub_k<kNo32>(cap, o));  // only on overflow, by the new amount
             }
             leaving = np_add_k<kNo32>(leaving, o);
             if (np_lt_k<kNo32>(pyint(0), snt))

@@ -45,6 +45,7 @@ struct LevelInbox {
   static constexpr bool kLdsSplit = false;
   static constexpr bool kVecActions = false;
   static constexpr bool kClearInAct = false;  // cleared before the act
+  static constexpr bool kShipBits = false;
   __host__ __device__ Num scratch_get(int) const { return pyint(0); }
   __host__ __device__ void noship(const ScCtx&, int, int, int) const {}
   __host__ __device__ void noship_all(const ScCtx&, int, int) const {}

@@ -80,6 +80,11 @@ struct StagedInbox {
   // noship_all: one store per destination and product in all), instead of a clear of the
   // node's every entry before it acts followed by the shipments' stores over most of them.
   static constexpr bool kClearInAct = SCG_STAGED_NOSHIP != 0;
+#ifndef SCG_STAGED_SHIP_BITS
+#define SCG_STAGED_SHIP_BITS 0
+#endif
+  // available_ship_capacities as overflow bits (ShipLeftBits): (P - 1) * MAXD <= 64
+  static constexpr bool kShipBits = SCG_STAGED_SHIP_BITS != 0;
   // the split's sorted values go to the amounts' slots (a float is exact in the double),
   // each read back before the amount of its rank overwrites it
   __host__ __device__ __forceinline__ void scratch_put_value(int s, float v) const {

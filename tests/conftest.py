@@ -11,7 +11,10 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PKG_ROOT = os.path.join(REPO, "gym-supplychain_amd")
+# SCG_PKG_ROOT=exp/NAME: run the suite against an experiment build (tools/exp_build.py)
+PKG_ROOT = os.environ.get("SCG_PKG_ROOT") or os.path.join(REPO, "gym-supplychain_amd")
+if not os.path.isabs(PKG_ROOT):
+    PKG_ROOT = os.path.join(REPO, PKG_ROOT)
 for p in (REPO, PKG_ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -13,17 +13,19 @@ OUT = os.path.join(REPO, "tests", "native", "_build", "libsc_host.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
 
-def build():
+def build(defines=()):
+    """The harness library; `defines` (e.g. ("SCG_STAGED_SHIP_BITS=1",)) build a variant of its own."""
+    out = OUT if not defines else OUT.replace(".so", "_" + "_".join(d.replace("=", "") for d in defines) + ".so")
     deps = [SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
         [os.path.join(REPO, "include", "scgpu.h")]
-    if not (os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps)):
-        os.makedirs(os.path.dirname(OUT), exist_ok=True)
-        tmp = f"{OUT}.{os.getpid()}.tmp"  # concurrent test workers: build aside, rename into place
+    if not (os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps)):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        tmp = f"{out}.{os.getpid()}.tmp"  # concurrent test workers: build aside, rename into place
         subprocess.run(["hipcc", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-Wno-pass-failed",
-                        "--offload-arch=gfx950", "-I", os.path.join(REPO, "include"), "-I", CSRC,
-                        "-o", tmp, SRC], check=True)
-        os.replace(tmp, OUT)
-    lib = ctypes.CDLL(OUT)
+                        "--offload-arch=gfx950", "-I", os.path.join(REPO, "include"), "-I", CSRC] +
+                       [f"-D{d}" for d in defines] + ["-o", tmp, SRC], check=True)
+        os.replace(tmp, out)
+    lib = ctypes.CDLL(out)
     lib.sch_episode.restype = ctypes.c_int
     lib.sch_episode_level.restype = ctypes.c_int
     lib.sch_episode_ledger.restype = ctypes.c_int

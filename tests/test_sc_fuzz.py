@@ -9,13 +9,21 @@ import pytest
 from sc_fuzz import oracle_for, random_actions, random_chain
 
 SEEDS = list(range(64))
-BODIES = ["lane", "level", "staged", "nodes", "nodes_serial"]
+BODIES = ["lane", "level", "staged", "nodes", "nodes_serial", "staged_shipbits"]
 
 
 @pytest.fixture(scope="module")
 def harness():
     import native_harness
     return native_harness.build()
+
+
+@pytest.fixture(scope="module")
+def harness_shipbits():
+    """The staged body with its ship capacities as overflow bits (ShipLeftBits,
+    SCG_STAGED_SHIP_BITS=1: a measured, not default, variant of the staged kernel)."""
+    import native_harness
+    return native_harness.build(("SCG_STAGED_SHIP_BITS=1",))
 
 
 def _prepare(nodes, env_kw, kernel):
@@ -43,7 +51,7 @@ def _prepare(nodes, env_kw, kernel):
 
 
 @pytest.mark.parametrize("seed", SEEDS)
-def test_random_chain_kernel_bodies_match_oracle(harness, seed):
+def test_random_chain_kernel_bodies_match_oracle(harness, harness_shipbits, seed):
     import native_harness
     from gym_supplychain_amd import _native as nat
     nodes, env_kw = random_chain(seed)
@@ -59,8 +67,9 @@ def test_random_chain_kernel_bodies_match_oracle(harness, seed):
         for env_id in (0, 5):
             o, obs0 = oracle_for(nodes, env_kw, draw_seed, env_id, 0, c.n_leadtimes)
             a = acts[:, 0 if env_id == 0 else 1]
+            lib = harness_shipbits if body == "staged_shipbits" else harness
             rc, obs, rew, *_ = native_harness.run_episode(
-                harness, c, table, thr, draw_seed, env_id, 0, a, level=body == "level", staged=body == "staged",
+                lib, c, table, thr, draw_seed, env_id, 0, a, level=body == "level", staged=body.startswith("staged"),
                 nodes_kernel=body.startswith("nodes"), nodes_serial=body == "nodes_serial")
             assert rc == 0, (seed, body)
             assert np.array_equal(obs[0], obs0), (seed, body, env_id)

@@ -101,11 +101,19 @@ def test_host_build_ledgers_match_reference(harness, name):
         assert np.allclose(np.cumsum(rew), g["led_rewards"][:, n], rtol=1e-12, atol=0)
 
 
+@pytest.fixture(scope="module")
+def harness_shipbits():
+    import native_harness
+    return native_harness.build(("SCG_STAGED_SHIP_BITS=1",))
+
+
+@pytest.mark.parametrize("shipbits", [False, True])
 @pytest.mark.parametrize("name", CASES)
-def test_host_build_of_staged_kernel_matches_reference(harness, name):
+def test_host_build_of_staged_kernel_matches_reference(harness, harness_shipbits, name, shipbits):
     """sc_step_staged_kernel's body (scg_supplychain_staged.h): one node's heaps staged at a
     time, shipments through the inbox — observations, rewards, stocks, heap storage order
-    and ledgers against the reference, exactly."""
+    and ledgers against the reference, exactly; also with the ship capacities kept as
+    overflow bits (SCG_STAGED_SHIP_BITS=1)."""
     import native_harness
     from gym_supplychain_amd import _native as nat
     g = load_sc(name)
@@ -115,7 +123,8 @@ def test_host_build_of_staged_kernel_matches_reference(harness, name):
     P = spec.P
     for n in range(g["obs"].shape[1]):
         rc, obs, rew, stock, (tk, val, size), (led_v, led_k) = native_harness.run_episode(
-            harness, c, nodes, thr, meta["seed"], n, 0, g["actions"][:, n], staged=True)
+            harness_shipbits if shipbits else harness, c, nodes, thr, meta["seed"], n, 0, g["actions"][:, n],
+            staged=True)
         assert rc == 0
         assert np.array_equal(obs, g["obs"][:, n]), name
         assert np.array_equal(rew, g["reward"][:, n]), name
