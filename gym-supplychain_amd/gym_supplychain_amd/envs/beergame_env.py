@@ -597,6 +597,10 @@ class BeerGameEnv(spaces.Env):
     and step() give int64 observations, step() an np.int64 reward, a bool done and {}
     (:138). Stepping past the last week raises IndexError (:79 on customer_demand[T]).
     The week runs on the GPU as a batch of one; use BeerGameVecEnv for throughput.
+    Each step is posted to a resident wave (the step server, include/scgpu.h
+    scg_bg_server_step) rather than launched; the wave exits 20 ms after the last step, on
+    reset() and on close(), so a device-wide torch.cuda.synchronize() right after a step
+    waits up to that long. SCG_BG_SERVER=0 launches the step kernel per step instead.
     State attributes (inventory, backlog, orders_placed, incoming_orders, shipments, the
     ledgers, all_orders_placed) are read back from the device when accessed.
     """
