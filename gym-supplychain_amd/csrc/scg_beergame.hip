@@ -489,6 +489,9 @@ int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server
   if (int rc = check_state(cfg, st)) return rc;
   if (!sv || !sv->box_host || !sv->box_dev || !sv->action || !sv->obs || !sv->reward)
     return fail(SCG_ERR_INVALID, "step server: mailbox, action, obs and reward are required");
+  // the wave stays resident between steps: on the null stream every blocking stream's work
+  // would wait for it to time out
+  if (!sv->stream) return fail(SCG_ERR_INVALID, "step server: needs a (non-blocking) stream of its own, not the null stream");
   if (st->n_envs > kServerBlock) return fail(SCG_ERR_INVALID, "the step server runs up to %d envs", kServerBlock);
   if (cfg->variant != 1) return fail(SCG_ERR_INVALID, "the step server runs BeerGameEnv (variant 1)");
   if (st->slab) return fail(SCG_ERR_INVALID, "the step server runs on separate state buffers (no slab)");

@@ -150,8 +150,8 @@ def test_step_rejects_shards_beyond_int32_before_any_launch():
 def test_step_server_validates_before_any_launch():
     """scg_bg_server_step / scg_bg_server_stop: every argument the resident wave depends on is
     checked on the host before anything is launched (more than 64 envs, BeerGameEnv2, the slab
-    layout, a missing mailbox or buffer, an idle time-out out of range, a step before reset or
-    past the horizon); stopping a server that never ran is a no-op."""
+    layout, a missing mailbox or buffer, the null stream, an idle time-out out of range, a step
+    before reset or past the horizon); stopping a server that never ran is a no-op."""
     from gym_supplychain_amd import _native as nat
     T = 35
     c = nat.BgConfig()
@@ -169,7 +169,7 @@ def test_step_server_validates_before_any_launch():
     for f in ("inventory", "backlog", "orders_placed", "shipments"):
         setattr(st, f, fake)
     box = nat.BgServerBox()
-    sv = nat.BgServer(ctypes.addressof(box), fake, fake, None, fake, fake, None, 20000, 0, 0, 0)
+    sv = nat.BgServer(ctypes.addressof(box), fake, fake, None, fake, fake, fake, 20000, 0, 0, 0)
     done = ctypes.c_int32(0)
 
     def step(expect, text):
@@ -182,6 +182,9 @@ def test_step_server_validates_before_any_launch():
     sv.obs = None
     step(nat.SCG_ERR_INVALID, "required")
     sv.obs = fake
+    sv.stream = None
+    step(nat.SCG_ERR_INVALID, "null stream")
+    sv.stream = fake
     sv.idle_us = 10
     step(nat.SCG_ERR_INVALID, "idle_us")
     sv.idle_us = 20000
