@@ -652,6 +652,9 @@ class SupplyChainEnv(spaces.Env):
     host_rng=False: Philox draws on the device from `seed` (module docstring).
     The reference's attributes `customer_demands`, `leadtimes`, `nodes` (SC_NodeView),
     `count_leadtimes_per_timestep` and `rand_generator` are kept.
+    kernel=None (default): the node-parallel kernel when the chain qualifies (one env is a
+    latency path: every node on its own wave), else the vec env's "auto" choice; or name one
+    ("lane", "staged", "level", "nodes", "auto").
     """
 
     def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
