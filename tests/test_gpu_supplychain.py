@@ -144,6 +144,29 @@ def test_single_env_facade_and_reference_known_answers():
         e.step(np.zeros(14, dtype=np.float32))
 
 
+@pytest.mark.parametrize("kernel", ["lane", "staged"])
+def test_single_env_kernel_choice_gives_the_same_episode(kernel):
+    """The drop-in env takes the node-parallel kernel by default (a latency choice, not the
+    batch occupancy rule); an explicitly named kernel runs the same episode: observations,
+    rewards and done, bit for bit, with the reference's host RandomState draws."""
+    from gym_supplychain_amd import SupplyChainEnv
+    from gym_supplychain_amd.envs.scenarios import two_per_stage_nodes
+    nodes, kw = two_per_stage_nodes(total_time_steps=40)
+    kw.pop("seed", None)
+    a = SupplyChainEnv(nodes, seed=11, device=DEV, **kw)
+    b = SupplyChainEnv(nodes, seed=11, device=DEV, kernel=kernel, **kw)
+    assert a._vec.kernel == "nodes" and b._vec.kernel == kernel
+    rng = np.random.RandomState(3)
+    for ep in range(2):
+        assert np.array_equal(a.reset(), b.reset())
+        done = False
+        while not done:
+            act = rng.uniform(-1, 1, a.action_space.shape).astype(np.float32)
+            o1, r1, done, _ = a.step(act)
+            o2, r2, d2, _ = b.step(act)
+            assert np.array_equal(o1, o2) and r1 == r2 and done == d2
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("scenario,n_envs,steps", [("sc-2perstage-v0", 65536, 6),
                                                    ("sc-Nperstage-multiproduct-v0", 262144, 2)])
