@@ -82,9 +82,10 @@ int launch_step(int L, dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo
   }
 }
 
-int launch_server(int L, hipStream_t s, const BgArgs& a, scg_bg_server_box* box, uint32_t last, uint32_t idle_ticks) {
+int launch_server(int L, int demand_mode, hipStream_t s, scg_bg_server_box* box, uint32_t exit_seen,
+                  uint32_t idle_ticks) {
   switch (L) {
-#define X(l) case l: return bg_launch_server<l>(s, a, box, last, idle_ticks);
+#define X(l) case l: return bg_launch_server<l>(s, demand_mode, box, exit_seen, idle_ticks);
     SCG_LEVEL_CASES(X)
 #undef X
     default: return fail(SCG_ERR_INVALID, "levels=%d outside 1..%d", L, SCG_BG_MAX_LEVELS);
@@ -426,7 +427,13 @@ int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const int32_t*
   return SCG_OK;
 }
 
-// ---- step server (include/scgpu.h: scg_bg_server_step) ----------------------------------
+// ---- step server (include/scgpu.h: scg_bg_server_*) -------------------------------------
+// the layouts the Python binding (_native.py) mirrors
+static_assert(sizeof(scg_bg_server_line) == 64, "request line");
+static_assert(sizeof(scg_bg_server_box) == 17 * 64 + 64 + SCG_BG_SERVER_SLOTS * SCG_BG_SERVER_ARGS_BYTES, "mailbox");
+static_assert(offsetof(scg_bg_server_box, done_seq) == 16 * 64 && offsetof(scg_bg_server_box, args) == 18 * 64,
+              "mailbox lines");
+static_assert(sizeof(scg_bg_server) == 72 && sizeof(scg_bg_server_slot) == 64, "server structs");
 static int64_t mono_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -439,35 +446,28 @@ static inline void cpu_relax() {
 #endif
 }
 
-// Post request `cmd`: the request line's words (plan, and the action row when it travels
-// inline) written first, then its check, then the new request number; returns that number.
-static uint32_t server_post(scg_bg_server_box* b, int32_t cmd, uint32_t wpack, int32_t week, int32_t demand_fixed,
-                            int32_t n_inline, const int32_t* act) {
-  uint32_t w[16] = {0};
-  const uint32_t seq = __atomic_load_n(&b->req_seq, __ATOMIC_RELAXED) + 1;
-  w[0] = seq;
-  w[1] = static_cast<uint32_t>(cmd);
-  w[2] = wpack;
-  w[3] = static_cast<uint32_t>(week);
-  w[4] = static_cast<uint32_t>(demand_fixed);
-  w[5] = static_cast<uint32_t>(n_inline);
-  for (int l = 0; l < n_inline; ++l) w[8 + l] = static_cast<uint32_t>(act[l]);
-  w[7] = server_line_check(w);
-  uint32_t* line = reinterpret_cast<uint32_t*>(b);
-  for (int i = 1; i < 16; ++i) __atomic_store_n(&line[i], w[i], __ATOMIC_RELAXED);
-  __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);
-  return seq;
-}
+// The server's host bookkeeping (launch, retire, slots, argument blocks) under a spin lock in
+// the struct itself: posts and waits of different slots may come from different threads.
+struct ServerLock {
+  int32_t* w;
+  explicit ServerLock(scg_bg_server* sv) : w(&sv->lock) {
+    for (;;) {
+      int32_t z = 0;
+      if (__atomic_compare_exchange_n(w, &z, 1, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) return;
+      cpu_relax();
+    }
+  }
+  ~ServerLock() { __atomic_store_n(w, 0, __ATOMIC_RELEASE); }
+};
 
-static int server_launch(const scg_bg_config* cfg, const scg_bg_state* st, scg_bg_server* sv) {
-  BgArgs a = make_args(cfg, st);
-  a.act = sv->action;
-  a.obs = sv->obs;
-  a.rew = sv->reward;
-  a.term_obs = nullptr;
-  const uint32_t last = __atomic_load_n(&sv->box_host->req_seq, __ATOMIC_ACQUIRE);
+static bool server_ok(const scg_bg_server* sv) { return sv && sv->box_host && sv->box_dev; }
+
+// Launch the wave (lock held). It serves, first, every slot whose request is newer than its answer.
+static int server_launch_locked(scg_bg_server* sv) {
+  const uint32_t exit_seen = __atomic_load_n(&sv->box_host->exit_req, __ATOMIC_ACQUIRE);
   const uint32_t idle_ticks = static_cast<uint32_t>(sv->idle_us) * 100u;  // 100 MHz real-time clock
-  if (int rc = launch_server(cfg->levels, static_cast<hipStream_t>(sv->stream), a, sv->box_dev, last, idle_ticks))
+  if (int rc = launch_server(sv->levels, sv->demand_mode, static_cast<hipStream_t>(sv->stream), sv->box_dev,
+                             exit_seen, idle_ticks))
     return rc;
   sv->running = 1;
   sv->launches += 1;
@@ -475,71 +475,178 @@ static int server_launch(const scg_bg_config* cfg, const scg_bg_state* st, scg_b
   return SCG_OK;
 }
 
-int scg_bg_server_stop(scg_bg_server* sv) {
-  if (!sv || !sv->box_host) return fail(SCG_ERR_INVALID, "null server/mailbox");
+static int server_stop_locked(scg_bg_server* sv) {
   if (!sv->running) return SCG_OK;
-  server_post(sv->box_host, 1, 0, 0, 0, 0, nullptr);
+  __atomic_store_n(&sv->box_host->exit_req, sv->box_host->exit_req + 1, __ATOMIC_RELEASE);
   sv->running = 0;
   if (hipStreamSynchronize(static_cast<hipStream_t>(sv->stream)) != hipSuccess)
     return fail(SCG_ERR_HIP, "step server: hipStreamSynchronize failed");
   return SCG_OK;
 }
 
-int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server* sv, int32_t* done) {
-  if (int rc = check_state(cfg, st)) return rc;
-  if (!sv || !sv->box_host || !sv->box_dev || !sv->action || !sv->obs || !sv->reward)
-    return fail(SCG_ERR_INVALID, "step server: mailbox, action, obs and reward are required");
-  // the wave stays resident between steps: on the null stream every blocking stream's work
-  // would wait for it to time out
+int scg_bg_server_stop(scg_bg_server* sv) {
+  if (!server_ok(sv)) return fail(SCG_ERR_INVALID, "null server/mailbox");
+  ServerLock lk(sv);
+  return server_stop_locked(sv);
+}
+
+uint32_t scg_bg_server_line_check(const scg_bg_server_line* line) {
+  uint32_t w[16];
+  std::memcpy(w, line, sizeof(w));
+  return server_line_check(w);
+}
+
+int scg_bg_server_attach(scg_bg_server* sv, scg_bg_server_slot* slot) {
+  if (!server_ok(sv) || !slot) return fail(SCG_ERR_INVALID, "null server/mailbox/slot");
+  if (!slot->action || !slot->obs || !slot->reward) return fail(SCG_ERR_INVALID, "step server: slot action, obs and reward are required");
   if (!sv->stream) return fail(SCG_ERR_INVALID, "step server: needs a (non-blocking) stream of its own, not the null stream");
-  if (st->n_envs > kServerBlock) return fail(SCG_ERR_INVALID, "the step server runs up to %d envs", kServerBlock);
+  if (sv->levels < 1 || sv->levels > SCG_BG_MAX_LEVELS) return fail(SCG_ERR_INVALID, "step server: levels=%d", sv->levels);
+  if (sv->demand_mode < SCG_DEMAND_FIXED || sv->demand_mode > SCG_DEMAND_UNIFORM)
+    return fail(SCG_ERR_INVALID, "step server: unknown demand_mode %d", sv->demand_mode);
+  if (sv->idle_us < 100 || sv->idle_us > 10000000) return fail(SCG_ERR_INVALID, "idle_us outside 100..10^7");
+  ServerLock lk(sv);
+  int k = 0;
+  while (k < kServerSlots && (sv->slots_used >> k & 1u)) ++k;
+  if (k == kServerSlots) return fail(SCG_ERR_INVALID, "step server: all %d slots are taken", kServerSlots);
+  scg_bg_server_box* b = sv->box_host;
+  sv->slots_used |= 1u << k;
+  slot->server = sv;
+  slot->index = k;
+  // a slot taken again continues its line's numbering; its arguments are published on the
+  // first post (cleared here, they differ from any real ones: a new generation)
+  slot->seq = __atomic_load_n(&b->req[k].req_seq, __ATOMIC_RELAXED);
+  slot->gen = b->req[k].gen;
+  std::memset(b->args[k], 0, sizeof(b->args[k]));
+  slot->week = 0;
+  slot->done = 0;
+  slot->relaunches = 0;
+  __atomic_store_n(&b->done_seq[k], slot->seq, __ATOMIC_RELEASE);
+  uint32_t ns = 0;
+  for (int j = 0; j < kServerSlots; ++j)
+    if (sv->slots_used >> j & 1u) ns = j + 1;
+  __atomic_store_n(&b->n_slots, ns, __ATOMIC_RELEASE);
+  return SCG_OK;
+}
+
+int scg_bg_server_detach(scg_bg_server_slot* slot) {
+  if (!slot || !server_ok(slot->server)) return fail(SCG_ERR_INVALID, "null slot or server");
+  scg_bg_server* sv = slot->server;
+  if (slot->index < 0) return SCG_OK;
+  scg_bg_server_box* b = sv->box_host;
+  const int k = slot->index;
+  if (__atomic_load_n(&b->done_seq[k], __ATOMIC_ACQUIRE) != slot->seq)
+    return fail(SCG_ERR_INVALID, "step server: detach with a request of slot %d unanswered", k);
+  ServerLock lk(sv);
+  sv->slots_used &= ~(1u << k);
+  uint32_t ns = 0;
+  for (int j = 0; j < kServerSlots; ++j)
+    if (sv->slots_used >> j & 1u) ns = j + 1;
+  __atomic_store_n(&b->n_slots, ns, __ATOMIC_RELEASE);
+  slot->index = -1;
+  return SCG_OK;
+}
+
+int scg_bg_server_post(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server_slot* slot) {
+  if (int rc = check_state(cfg, st)) return rc;
+  if (!slot || !server_ok(slot->server) || slot->index < 0 || slot->index >= kServerSlots)
+    return fail(SCG_ERR_INVALID, "step server: the slot is not attached");
+  scg_bg_server* sv = slot->server;
+  if (st->n_envs > kServerBlock) return fail(SCG_ERR_INVALID, "the step server runs up to %d envs per slot", kServerBlock);
   if (cfg->variant != 1) return fail(SCG_ERR_INVALID, "the step server runs BeerGameEnv (variant 1)");
   if (st->slab) return fail(SCG_ERR_INVALID, "the step server runs on separate state buffers (no slab)");
-  if (sv->idle_us < 100 || sv->idle_us > 10000000) return fail(SCG_ERR_INVALID, "idle_us outside 100..10^7");
+  if (cfg->levels != sv->levels || cfg->demand_mode != sv->demand_mode)
+    return fail(SCG_ERR_INVALID, "step server: the config (levels %d, demand mode %d) is not the server's (%d, %d)",
+                cfg->levels, cfg->demand_mode, sv->levels, sv->demand_mode);
   if (int rc = check_step(cfg, st)) return rc;
+  scg_bg_server_box* b = sv->box_host;
+  const int k = slot->index;
+  if (__atomic_load_n(&b->done_seq[k], __ATOMIC_ACQUIRE) != slot->seq)
+    return fail(SCG_ERR_INVALID, "step server: slot %d posts while its last request is unanswered", k);
   const int32_t w = st->week + 1;
   const WeekInfo wk = week_info(cfg, w, 0);
+  BgArgs a = make_args(cfg, st);
+  a.act = slot->action;
+  a.obs = slot->obs;
+  a.rew = slot->reward;
+  a.term_obs = nullptr;
+  ServerLock lk(sv);
+  // the slot's arguments: a new generation whenever they differ from the published ones (the
+  // wave reloads them only then; nothing of the slot is in flight, so rewriting is safe)
+  if (std::memcmp(b->args[k], &a, sizeof(a)) != 0) {
+    std::memcpy(b->args[k], &a, sizeof(a));
+    slot->gen = slot->gen + 1 ? slot->gen + 1 : 1;  // 0 is the wave's "none loaded"
+  }
   // a wave idle for more than half its time-out may be exiting: retire it before posting
   if (sv->running && mono_ns() - sv->last_ns > static_cast<int64_t>(sv->idle_us) * 500)
-    if (int rc = scg_bg_server_stop(sv)) return rc;
+    if (int rc = server_stop_locked(sv)) return rc;
+  uint32_t line[16] = {0};
+  const uint32_t seq = slot->seq + 1;
+  const int32_t n_inline = (slot->action_host && st->n_envs == 1 && cfg->levels <= 8) ? cfg->levels : 0;
+  line[0] = seq;
+  line[2] = pack_week(wk);
+  line[3] = static_cast<uint32_t>(w);
+  line[4] = static_cast<uint32_t>(wk.demand_fixed);
+  line[5] = static_cast<uint32_t>(n_inline);
+  line[6] = slot->gen;
+  for (int l = 0; l < n_inline; ++l) line[8 + l] = static_cast<uint32_t>(slot->action_host[l]);
+  line[7] = server_line_check(line);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&b->req[k]);
+  for (int i = 1; i < 16; ++i) __atomic_store_n(&dst[i], line[i], __ATOMIC_RELAXED);
+  __atomic_store_n(&dst[0], seq, __ATOMIC_RELEASE);
+  slot->seq = seq;
+  slot->week = w;
+  slot->done = (wk.flags & 1) ? 1 : 0;
+  sv->last_ns = mono_ns();
+  if (!sv->running)
+    if (int rc = server_launch_locked(sv)) return rc;
+  return SCG_OK;
+}
+
+int scg_bg_server_wait(scg_bg_state* st, scg_bg_server_slot* slot, int64_t spin_us, int32_t* done) {
+  if (!st || !slot || !server_ok(slot->server) || slot->index < 0 || slot->index >= kServerSlots)
+    return fail(SCG_ERR_INVALID, "step server: the slot is not attached");
+  scg_bg_server* sv = slot->server;
   scg_bg_server_box* b = sv->box_host;
-  // Waiting for the answer, every 2 s: a wave that has exited without serving the request
-  // (its stream is idle: e.g. a host stall past its time-out) is launched again and the week
-  // posted again, once; a wave still queued or running is waited for, up to 60 s in all (a
-  // busy GPU may start it late).
+  const int k = slot->index;
+  const uint32_t seq = slot->seq;
   const int64_t start = mono_ns();
-  for (int relaunched = 0;;) {
-    if (!sv->running)
-      if (int rc = server_launch(cfg, st, sv)) return rc;
-    const int32_t n_inline = (sv->action_host && st->n_envs == 1 && cfg->levels <= 8) ? cfg->levels : 0;
-    const uint32_t seq = server_post(b, 0, pack_week(wk), w, wk.demand_fixed, n_inline, sv->action_host);
-    bool served = false, gone = false;
-    int64_t check = mono_ns() + 2000000000;
-    for (uint32_t spins = 0;; ++spins) {
-      if (__atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) == seq) {
-        served = true;
-        break;
-      }
-      cpu_relax();
-      if ((spins & 1023u) != 1023u) continue;
-      const int64_t now = mono_ns();
-      if (now < check) continue;
-      check = now + 2000000000;
-      if (hipStreamQuery(static_cast<hipStream_t>(sv->stream)) == hipSuccess &&
-          __atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq) {
-        gone = true;
-        break;
-      }
-      if (now - start > 60000000000LL) return fail(SCG_ERR_HIP, "step server: no answer for 60 s (week %d)", w);
+  const int64_t check_ns = (sv->check_us > 0 ? sv->check_us : 2000000) * int64_t(1000);
+  int64_t check = start + check_ns;
+  int gone = 0;
+  for (uint32_t spins = 0;; ++spins) {
+    if (__atomic_load_n(&b->done_seq[k], __ATOMIC_ACQUIRE) == seq) break;
+    cpu_relax();
+    if ((spins & 255u) != 255u) continue;
+    const int64_t now = mono_ns();
+    if (spin_us >= 0 && now - start > spin_us * 1000) return SCG_PENDING;
+    if (now < check) continue;
+    check = now + check_ns;
+    // Every check interval: a wave that has exited without serving the request (its stream
+    // idle: a host stall past its time-out, an exit another thread asked for) is launched
+    // again — it serves pending requests first — once per wait; a HIP error on the stream
+    // fails at once; a wave still queued or running is waited for, up to 60 s in all.
+    ServerLock lk(sv);
+    const hipError_t q = hipStreamQuery(static_cast<hipStream_t>(sv->stream));
+    if (q != hipSuccess && q != hipErrorNotReady)
+      return fail(SCG_ERR_HIP, "step server: the wave's stream reports %s (week %d)", hipGetErrorString(q), slot->week);
+    if (__atomic_load_n(&b->done_seq[k], __ATOMIC_ACQUIRE) == seq) break;
+    if (q == hipSuccess) {
+      if (gone++ > 0) return fail(SCG_ERR_HIP, "step server: the wave exits without answering (week %d)", slot->week);
+      sv->running = 0;
+      slot->relaunches += 1;
+      if (int rc = server_launch_locked(sv)) return rc;
     }
-    if (served) break;
-    if (gone && relaunched++ > 0) return fail(SCG_ERR_HIP, "step server: the wave exits without answering (week %d)", w);
-    sv->running = 0;
+    if (now - start > 60000000000LL) return fail(SCG_ERR_HIP, "step server: no answer for 60 s (week %d)", slot->week);
   }
   sv->last_ns = mono_ns();
-  st->week = w;  // no auto-reset on this path
-  if (done) *done = (wk.flags & 1) ? 1 : 0;
+  st->week = slot->week;  // no auto-reset on this path
+  if (done) *done = slot->done;
   return SCG_OK;
+}
+
+int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server_slot* slot, int32_t* done) {
+  if (int rc = scg_bg_server_post(cfg, st, slot)) return rc;
+  return scg_bg_server_wait(st, slot, -1, done);
 }
 
 int scg_bg_rollout(const scg_bg_config* cfg, scg_bg_state* st, int32_t n_weeks, const int32_t* actions,

@@ -555,62 +555,120 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
   bg_step_env<L, DM>(n, inv_p, bk_p, op_p, act_p, ring_p, n32, wpack, a, wk);
 }
 
-// ---- step server (scg_bg_server_step: the drop-in BeerGameEnv) ----------------------------
-// The request is one 64-byte line of the mailbox (scg_bg_server_box): 16 words, word 7 the
-// check over the others (include/scgpu.h), so a read that mixes two requests is detected.
+// ---- step server (scg_bg_server_*: the drop-in BeerGameEnv) -------------------------------
+// A request is one 64-byte line of the mailbox (scg_bg_server_line): 16 words, word 7 a mixing
+// hash of the other 15 (multiply, xor, rotate per word), so a read that mixes two requests is
+// detected whatever the words' differences.
 __host__ __device__ inline uint32_t server_line_check(const uint32_t (&w)[16]) {
-  uint32_t c = 0x9E3779B9u;
-  for (int i = 0; i < 16; ++i)
-    if (i != 7) c += w[i] * static_cast<uint32_t>(2 * i + 1);
-  return c;
+  uint32_t h = 0x9E3779B9u;
+  for (int i = 0; i < 16; ++i) {
+    if (i == 7) continue;
+    h ^= w[i] * 0x85EBCA6Bu + static_cast<uint32_t>(i);
+    h = (h << 13) | (h >> 19);
+    h = h * 5u + 0xE6546B64u;
+  }
+  h ^= h >> 16;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 13);
 }
 
-// One wave, env n on lane n (a.n <= 64). Lanes 0-15 read the request line in one load
-// (system scope: past the caches, from host memory); on a new, consistent request the wave
-// runs the week body above with the posted plan — with env 0's action row from the line
-// itself when n_inline says it travelled there — then publishes the request number with a
-// system-scope release store after every lane's stores. It exits on cmd != 0, or when no
-// request has come for idle_ticks of the 100 MHz real-time clock, so it never outlives its
-// host process.
 constexpr int kServerBlock = 64;
+constexpr int kServerSlots = SCG_BG_SERVER_SLOTS;
+constexpr int kServerArgWords = (sizeof(BgArgs) + 15) / 16 * 4;  // rows 16-byte aligned
+static_assert(sizeof(BgArgs) <= SCG_BG_SERVER_ARGS_BYTES, "BgArgs outgrew the mailbox's argument blocks");
+static_assert(kServerSlots <= 16 && kServerArgWords <= 2 * kServerBlock, "server layout");
+
+// One wave serves every slot of the mailbox: env n of a slot on lane n (a slot's a.n <= 64).
+// Each poll reads the request lines of slots 0 .. n_slots - 1 in up to four loads (lane l
+// reads word l % 16 of slot 4r + l / 16; system scope: past the caches, from host memory)
+// together with the control words; for every slot whose line carries a new, consistent request the wave loads
+// the slot's kernel arguments into LDS if their generation changed, runs the week body above
+// with the posted plan — env 0's action row from the line itself when n_inline says it
+// travelled there — and publishes the request number in the slot's answer word with a
+// system-scope release store after every lane's stores. At launch every slot's last served
+// request is its answer word, so requests posted while no wave ran are served first. It exits
+// when exit_req changes, or when no request has come for idle_ticks of the 100 MHz real-time
+// clock, so it never outlives its host process; as it exits it writes the exit word it saw.
 template <int L, int DM>
-__global__ __launch_bounds__(kServerBlock) void bg_server_kernel(const BgArgs a, scg_bg_server_box* box, uint32_t last,
+__global__ __launch_bounds__(kServerBlock) void bg_server_kernel(scg_bg_server_box* box, uint32_t exit_seen,
                                                                  uint32_t idle_ticks) {
-  const int64_t n = threadIdx.x;
-  const uint32_t* line = reinterpret_cast<const uint32_t*>(box);
+  __shared__ __align__(16) uint32_t s_args[kServerSlots][kServerArgWords];
+  __shared__ uint32_t s_last[16], s_gen[16];
+  const int lane = threadIdx.x;
+  if (lane < 16) {
+    s_last[lane] = __hip_atomic_load(&box->done_seq[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_gen[lane] = 0;  // hosts publish generations from 1
+  }
+  __syncthreads();
+  const uint32_t* lines = reinterpret_cast<const uint32_t*>(box->req);
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t ex = exit_seen;
+  // the slot count a poll reads lines by is the one the previous poll read (requested beside
+  // the lines, so a poll is one round trip to host memory): a slot attached since is polled
+  // one round later
+  uint32_t ns = __hip_atomic_load(&box->n_slots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
-    const uint32_t v = __hip_atomic_load(line + (threadIdx.x & 15u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t w[16];
+    const int n_slots = __builtin_amdgcn_readfirstlane(static_cast<int>(ns < kServerSlots ? ns : kServerSlots));
+    ns = __hip_atomic_load(&box->n_slots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    ex = __hip_atomic_load(&box->exit_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t v[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_readlane(v, i);
-    if (w[0] == last || w[7] != server_line_check(w)) {  // nothing new (or a torn read: again)
-      if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
-      __builtin_amdgcn_s_sleep(2);
+    for (int r = 0; r < 4; ++r) {
+      const int slot = 4 * r + (lane >> 4);
+      if (slot < n_slots)
+        v[r] = __hip_atomic_load(lines + slot * 16 + (lane & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    bool served = false;
+    for (int slot = 0; slot < n_slots; ++slot) {
+      const int base = (slot & 3) * 16, r = slot >> 2;
+      const uint32_t vr = r == 0 ? v[0] : r == 1 ? v[1] : r == 2 ? v[2] : v[3];
+      const uint32_t seq = __builtin_amdgcn_readlane(vr, base);
+      if (seq == s_last[slot]) continue;
+      uint32_t w[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_readlane(vr, base + i);
+      if (w[7] != server_line_check(w)) continue;  // a torn read: the next poll reads it again
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (w[6] != s_gen[slot]) {  // the slot's arguments changed (a new env or a reset): reload
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(box->args[slot]);
+        for (int k = lane; k < kServerArgWords; k += kServerBlock)
+          s_args[slot][k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        if (lane == 0) s_gen[slot] = w[6];
+      }
+      const BgArgs& a = *reinterpret_cast<const BgArgs*>(s_args[slot]);
+      WeekInfo wk{};
+      wk.week = static_cast<int32_t>(w[3]);
+      wk.demand_fixed = static_cast<int32_t>(w[4]);
+      const int64_t n = lane;
+      if (n < a.n) {
+        if (L <= 8 && static_cast<int32_t>(w[5]) == L) {  // the action row came with the request
+          int32_t act_in[L];
+#pragma unroll
+          for (int l = 0; l < L; ++l) act_in[l] = static_cast<int32_t>(w[8 + (l < 8 ? l : 0)]);
+          bg_step_env<L, DM, true>(n, a.inv, a.bk, a.op, a.act, a.ring, static_cast<uint32_t>(a.n), w[2], a, wk, act_in);
+        } else {
+          bg_step_env<L, DM>(n, a.inv, a.bk, a.op, a.act, a.ring, static_cast<uint32_t>(a.n), w[2], a, wk);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every lane's stores before the answer
+      if (lane == 0) {
+        __hip_atomic_store(&box->done_seq[slot], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_last[slot] = seq;
+      }
+      __syncthreads();
+      served = true;
+    }
+    if (ex != exit_seen) break;
+    if (served) {
+      t0 = __builtin_amdgcn_s_memrealtime();
       continue;
     }
-    last = w[0];
-    if (w[1] != 0) break;  // cmd: exit
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    WeekInfo wk{};
-    wk.week = static_cast<int32_t>(w[3]);
-    wk.demand_fixed = static_cast<int32_t>(w[4]);
-    if (n < a.n) {
-      if (L <= 8 && static_cast<int32_t>(w[5]) == L) {  // the action row came with the request
-        int32_t act_in[L];
-#pragma unroll
-        for (int l = 0; l < L; ++l) act_in[l] = static_cast<int32_t>(w[8 + (l < 8 ? l : 0)]);
-        bg_step_env<L, DM, true>(n, a.inv, a.bk, a.op, a.act, a.ring, static_cast<uint32_t>(a.n), w[2], a, wk, act_in);
-      } else {
-        bg_step_env<L, DM>(n, a.inv, a.bk, a.op, a.act, a.ring, static_cast<uint32_t>(a.n), w[2], a, wk);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every lane's stores before the answer
-    if (threadIdx.x == 0) __hip_atomic_store(&box->done_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    t0 = __builtin_amdgcn_s_memrealtime();
+    if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+    __builtin_amdgcn_s_sleep(2);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  if (threadIdx.x == 0) __hip_atomic_store(&box->exit_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) __hip_atomic_store(&box->exit_seq, ex, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- slab step kernel -------------------------------------------------------------------
@@ -1055,23 +1113,23 @@ int bg_launch_step(dim3 grid, hipStream_t s, const BgArgs& a, const WeekInfo& wk
 }
 
 template <int L>
-int bg_launch_server(hipStream_t s, const BgArgs& a, scg_bg_server_box* box, uint32_t last, uint32_t idle_ticks) {
-  switch (a.demand_mode) {
+int bg_launch_server(hipStream_t s, int demand_mode, scg_bg_server_box* box, uint32_t exit_seen, uint32_t idle_ticks) {
+  switch (demand_mode) {
     case SCG_DEMAND_FIXED:
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_FIXED>), dim3(1), dim3(kServerBlock), 0, s, a, box,
-                         last, idle_ticks);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_FIXED>), dim3(1), dim3(kServerBlock), 0, s, box,
+                         exit_seen, idle_ticks);
       break;
     case SCG_DEMAND_TABLE:
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_TABLE>), dim3(1), dim3(kServerBlock), 0, s, a, box,
-                         last, idle_ticks);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_TABLE>), dim3(1), dim3(kServerBlock), 0, s, box,
+                         exit_seen, idle_ticks);
       break;
     case SCG_DEMAND_UNIFORM:
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_UNIFORM>), dim3(1), dim3(kServerBlock), 0, s, a,
-                         box, last, idle_ticks);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_UNIFORM>), dim3(1), dim3(kServerBlock), 0, s, box,
+                         exit_seen, idle_ticks);
       break;
     default:
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_POISSON>), dim3(1), dim3(kServerBlock), 0, s, a,
-                         box, last, idle_ticks);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(bg_server_kernel<L, SCG_DEMAND_POISSON>), dim3(1), dim3(kServerBlock), 0, s, box,
+                         exit_seen, idle_ticks);
   }
   return check_launch("bg_server_kernel");
 }
@@ -1128,7 +1186,7 @@ int bg_launch_rollout(dim3 grid, hipStream_t s, const BgArgs& a, int32_t K, cons
   EXT template int bg_launch_reset<l>(dim3, hipStream_t, const BgArgs&);                                            \
   EXT template int bg_launch_step2<l>(dim3, hipStream_t, const BgArgs&, const WeekInfo&);                           \
   EXT template int bg_launch_step<l>(dim3, hipStream_t, const BgArgs&, const WeekInfo&, hipEvent_t, hipEvent_t);    \
-  EXT template int bg_launch_server<l>(hipStream_t, const BgArgs&, scg_bg_server_box*, uint32_t, uint32_t);         \
+  EXT template int bg_launch_server<l>(hipStream_t, int, scg_bg_server_box*, uint32_t, uint32_t);                   \
   EXT template int bg_launch_slab<l>(int, dim3, hipStream_t, int32_t*, const int32_t*, int32_t*, uint32_t, uint32_t, \
                                      uint32_t, uint32_t, uint32_t, uint32_t, const BgSlabArgs&, hipEvent_t,         \
                                      hipEvent_t);                                                                    \

@@ -90,7 +90,9 @@ static PyObject* bg_step_timed(PyObject* self, PyObject* const* args, Py_ssize_t
   return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
 }
 
-/* bg_server_step(cfg, state, server): one week through the step server (scg_bg_server_step) */
+/* bg_server_step(cfg, state, slot): one week through the step server — post, spin up to
+ * 200 us holding the GIL (the answer usually comes in a few), then wait with the GIL released
+ * (other Python threads run; the C wait fails after 60 s or on a HIP error of the wave's stream). */
 static PyObject* bg_server_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
   (void)self;
   void* p[3];
@@ -100,8 +102,16 @@ static PyObject* bg_server_step(PyObject* self, PyObject* const* args, Py_ssize_
   }
   for (int i = 0; i < 3; ++i)
     if (as_ptr(args[i], &p[i])) return NULL;
+  scg_bg_state* st = (scg_bg_state*)p[1];
+  scg_bg_server_slot* slot = (scg_bg_server_slot*)p[2];
   int32_t done = 0;
-  const int rc = scg_bg_server_step((const scg_bg_config*)p[0], (scg_bg_state*)p[1], (scg_bg_server*)p[2], &done);
+  int rc = scg_bg_server_post((const scg_bg_config*)p[0], st, slot);
+  if (rc == SCG_OK) rc = scg_bg_server_wait(st, slot, 200, &done);
+  if (rc == SCG_PENDING) {
+    Py_BEGIN_ALLOW_THREADS
+    rc = scg_bg_server_wait(st, slot, -1, &done);
+    Py_END_ALLOW_THREADS
+  }
   return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
 }
 

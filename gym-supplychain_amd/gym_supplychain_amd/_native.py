@@ -16,13 +16,14 @@ import torch  # noqa: F401  (loads the HIP runtime libscgpu.so binds to)
 
 LIB_NAME = "libscgpu.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 SCG_OK = 0
 SCG_ERR_INVALID = 1
 SCG_ERR_PAST_HORIZON = 2
 SCG_ERR_NOT_RESET = 3
 SCG_ERR_HIP = 4
+SCG_PENDING = 5  # scg_bg_server_wait: not answered yet (not an error)
 
 SCG_DEMAND_FIXED = 0
 SCG_DEMAND_TABLE = 1
@@ -101,20 +102,40 @@ class BgState(ctypes.Structure):
     ]
 
 
-class BgServerBox(ctypes.Structure):
-    """scg_bg_server_box (include/scgpu.h): the step server's mailbox, in host-mapped memory."""
+BG_SERVER_SLOTS = 15
+BG_SERVER_ARGS_BYTES = 512
+
+
+class BgServerLine(ctypes.Structure):
+    """scg_bg_server_line (include/scgpu.h): one slot's 64-byte request line."""
     _fields_ = [("req_seq", ctypes.c_uint32), ("cmd", ctypes.c_int32), ("wpack", ctypes.c_uint32),
                 ("week", ctypes.c_int32), ("demand_fixed", ctypes.c_int32), ("n_inline", ctypes.c_int32),
-                ("pad0", ctypes.c_int32), ("check", ctypes.c_uint32), ("action", ctypes.c_int32 * 8),
-                ("done_seq", ctypes.c_uint32), ("exit_seq", ctypes.c_uint32), ("pad1", ctypes.c_int32 * 14)]
+                ("gen", ctypes.c_uint32), ("check", ctypes.c_uint32), ("action", ctypes.c_int32 * 8)]
+
+
+class BgServerBox(ctypes.Structure):
+    """scg_bg_server_box (include/scgpu.h): the step server's mailbox, in host-mapped memory."""
+    _fields_ = [("req", BgServerLine * (BG_SERVER_SLOTS + 1)), ("done_seq", ctypes.c_uint32 * 16),
+                ("n_slots", ctypes.c_uint32), ("exit_req", ctypes.c_uint32), ("exit_seq", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32 * 13),
+                ("args", (ctypes.c_ubyte * BG_SERVER_ARGS_BYTES) * BG_SERVER_SLOTS)]
 
 
 class BgServer(ctypes.Structure):
-    """scg_bg_server (include/scgpu.h): the step server's launch arguments and host bookkeeping."""
-    _fields_ = [("box_host", ctypes.c_void_p), ("box_dev", ctypes.c_void_p), ("action", ctypes.c_void_p),
-                ("action_host", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p),
-                ("stream", ctypes.c_void_p), ("idle_us", ctypes.c_int32), ("running", ctypes.c_int32),
-                ("last_ns", ctypes.c_int64), ("launches", ctypes.c_int64)]
+    """scg_bg_server (include/scgpu.h): one resident wave serving up to BG_SERVER_SLOTS envs."""
+    _fields_ = [("box_host", ctypes.c_void_p), ("box_dev", ctypes.c_void_p), ("stream", ctypes.c_void_p),
+                ("levels", ctypes.c_int32), ("demand_mode", ctypes.c_int32), ("idle_us", ctypes.c_int32),
+                ("check_us", ctypes.c_int32), ("lock", ctypes.c_int32), ("running", ctypes.c_int32),
+                ("slots_used", ctypes.c_uint32), ("pad", ctypes.c_int32), ("last_ns", ctypes.c_int64),
+                ("launches", ctypes.c_int64)]
+
+
+class BgServerSlot(ctypes.Structure):
+    """scg_bg_server_slot (include/scgpu.h): one env's slot of a step server."""
+    _fields_ = [("server", ctypes.c_void_p), ("action", ctypes.c_void_p), ("action_host", ctypes.c_void_p),
+                ("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("index", ctypes.c_int32),
+                ("gen", ctypes.c_uint32), ("seq", ctypes.c_uint32), ("week", ctypes.c_int32),
+                ("done", ctypes.c_int32), ("relaunches", ctypes.c_int32)]
 
 
 # scg_bg_slab_field: word offsets of a BeerGame state slab (scg_bg_slab_layout)
@@ -198,9 +219,16 @@ SIGNATURES = {
     "scg_bg_step_timed": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          _i32p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "scg_bg_server_attach": (ctypes.c_int, [ctypes.POINTER(BgServer), ctypes.POINTER(BgServerSlot)]),
+    "scg_bg_server_detach": (ctypes.c_int, [ctypes.POINTER(BgServerSlot)]),
+    "scg_bg_server_post": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState),
+                                          ctypes.POINTER(BgServerSlot)]),
+    "scg_bg_server_wait": (ctypes.c_int, [ctypes.POINTER(BgState), ctypes.POINTER(BgServerSlot), ctypes.c_int64,
+                                          _i32p]),
     "scg_bg_server_step": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState),
-                                          ctypes.POINTER(BgServer), _i32p]),
+                                          ctypes.POINTER(BgServerSlot), _i32p]),
     "scg_bg_server_stop": (ctypes.c_int, [ctypes.POINTER(BgServer)]),
+    "scg_bg_server_line_check": (ctypes.c_uint32, [ctypes.POINTER(BgServerLine)]),
     "scg_bg_rollout": (ctypes.c_int, [ctypes.POINTER(BgConfig), ctypes.POINTER(BgState), ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p]),

@@ -531,43 +531,64 @@ class BeerGameVecEnv:
         pass
 
 
-_SERVERS = weakref.WeakSet()
+_SERVERS = {}  # (device index, levels, demand mode) -> _StepServer, one resident wave each
 
 
 @atexit.register
 def _stop_servers():  # no step-server wave outlives the interpreter (nor its mailbox)
-    for sv in list(_SERVERS):
+    for sv in list(_SERVERS.values()):
         sv.close()
 
 
 class _StepServer:
-    """The drop-in env's step server (include/scgpu.h scg_bg_server_step): one wave on a
-    non-blocking stream of its own polls a mailbox in host-mapped memory and runs each posted
-    week on the vec env's state. It exits when stopped, or by itself after IDLE_US without a
-    request; step() launches it again when needed. The mailbox is this object's own, freed
-    only after the wave has been stopped (the wave reads nothing else while it waits)."""
+    """A step server (include/scgpu.h scg_bg_server_*): one wave on a non-blocking,
+    high-priority stream of its own polls a mailbox in host-mapped memory and runs each week
+    an attached env posts on that env's state. One per (device, levels, demand mode) in a
+    process, whatever the number of drop-in envs (up to BG_SERVER_SLOTS per server; more
+    start another server): many envs stepped in turn share one resident wave and one stream.
+    The high priority puts the stream on a hardware queue of its own pool, so the parked wave
+    never holds up work of normal-priority streams that would share its queue. The wave exits
+    when stopped, or by itself after IDLE_US without a request; a post launches it again when
+    needed. The mailbox is freed only after the wave has been stopped."""
 
     IDLE_US = 20000
 
-    def __init__(self, vec, act_dev, act_host, obs_dev, rew_dev):
+    @classmethod
+    def attach(cls, vec, act_dev, act_host, obs_dev, rew_dev):
+        """A slot of this process's server for `vec` (a free one, or a new server)."""
+        key0 = (vec._dev_index, int(vec._cfg.levels), int(vec._cfg.demand_mode))
+        for j in range(64):
+            key = key0 + (j,)
+            sv = _SERVERS.get(key)
+            if sv is None:
+                sv = _SERVERS[key] = cls(vec.device, key0[1], key0[2], key)
+            if bin(sv.sv.slots_used).count("1") < nat.BG_SERVER_SLOTS:
+                return _ServerSlot(sv, vec, act_dev, act_host, obs_dev, rew_dev)
+        raise RuntimeError("too many drop-in envs on one device for the step server")
+
+    def __init__(self, device, levels, demand_mode, key):
         hip = nat.hip_runtime()
-        hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        hip.hipStreamCreateWithPriority.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint, ctypes.c_int]
+        hip.hipDeviceGetStreamPriorityRange.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
         stream = ctypes.c_void_p()
-        with torch.cuda.device(vec.device):
-            if hip.hipStreamCreateWithFlags(ctypes.byref(stream), 1) != 0:  # hipStreamNonBlocking
-                raise RuntimeError("hipStreamCreateWithFlags failed")
-        self._hip, self._vec, self._device = hip, vec, vec.device
+        with torch.cuda.device(device):
+            least, greatest = ctypes.c_int(0), ctypes.c_int(0)
+            if hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest)) != 0:
+                greatest.value = 0
+            # hipStreamNonBlocking, the highest priority the device offers
+            if hip.hipStreamCreateWithPriority(ctypes.byref(stream), 1, greatest.value) != 0:
+                raise RuntimeError("hipStreamCreateWithPriority failed")
+        self._hip, self._device, self._key = hip, device, key
+        self.priority = greatest.value
         self._box = box = nat.MappedBuffer(ctypes.sizeof(nat.BgServerBox))
-        self.sv = nat.BgServer(box.host, box.dev, act_dev, act_host, obs_dev, rew_dev, stream.value, self.IDLE_US, 0, 0,
-                               0)
-        self._args = (vec._cfg_addr, vec._st_addr, ctypes.addressof(self.sv))
-        self._fast = nat.fast.bg_server_step
+        self.box = nat.BgServerBox.from_address(box.host)
+        self.sv = nat.BgServer(box.host, box.dev, stream.value, levels, demand_mode, self.IDLE_US, 0)
         self._closed = False
-        _SERVERS.add(self)
 
-    def step(self):
-        return self._fast(*self._args)
+    @property
+    def launches(self):
+        return int(self.sv.launches)
 
     def stop(self):
         if not self._closed:
@@ -581,7 +602,31 @@ class _StepServer:
         self._closed = True
         self._hip.hipStreamDestroy(ctypes.c_void_p(self.sv.stream))
         self._box = None
-        _SERVERS.discard(self)
+        if _SERVERS.get(self._key) is self:
+            del _SERVERS[self._key]
+
+
+class _ServerSlot:
+    """One drop-in env's slot of a _StepServer: step() posts the env's week and returns once
+    the wave has written its observation and reward (scg_pybind.c bg_server_step)."""
+
+    def __init__(self, server, vec, act_dev, act_host, obs_dev, rew_dev):
+        self.server = server
+        self.slot = nat.BgServerSlot(None, act_dev, act_host, obs_dev, rew_dev, -1)
+        nat.check(nat.lib.scg_bg_server_attach(ctypes.byref(server.sv), ctypes.byref(self.slot)))
+        self._args = (vec._cfg_addr, vec._st_addr, ctypes.addressof(self.slot))
+        self._fast = nat.fast.bg_server_step
+
+    @property
+    def sv(self):
+        return self.server.sv
+
+    def step(self):
+        return self._fast(*self._args)
+
+    def close(self):
+        if self.slot.index >= 0 and not self.server._closed:
+            nat.check(nat.lib.scg_bg_server_detach(ctypes.byref(self.slot)))
 
     def __del__(self):
         try:
@@ -598,9 +643,10 @@ class BeerGameEnv(spaces.Env):
     (:138). Stepping past the last week raises IndexError (:79 on customer_demand[T]).
     The week runs on the GPU as a batch of one; use BeerGameVecEnv for throughput.
     Each step is posted to a resident wave (the step server, include/scgpu.h
-    scg_bg_server_step) rather than launched; the wave exits 20 ms after the last step, on
-    reset() and on close(), so a device-wide torch.cuda.synchronize() right after a step
-    waits up to that long. SCG_BG_SERVER=0 launches the step kernel per step instead.
+    scg_bg_server_*) rather than launched; every drop-in env of the process with the same
+    levels on the same device shares that one wave (a slot each). The wave exits 20 ms after
+    the last step of any of them, so a device-wide torch.cuda.synchronize() right after a
+    step waits up to that long. SCG_BG_SERVER=0 launches the step kernel per step instead.
     State attributes (inventory, backlog, orders_placed, incoming_orders, shipments, the
     ledgers, all_orders_placed) are read back from the device when accessed.
     """
@@ -643,7 +689,7 @@ class BeerGameEnv(spaces.Env):
         # step kernel plus one synchronisation per step instead.
         self._server = None
         if os.environ.get("SCG_BG_SERVER", "1") != "0":
-            self._server = _StepServer(self._vec, self._act_dev, io.host + 16, obs_dev, rew_dev)
+            self._server = _StepServer.attach(self._vec, self._act_dev, io.host + 16, obs_dev, rew_dev)
         self._step_args = nat.BgStepArgs(vec._cfg_addr, vec._st_addr, obs_dev, rew_dev, vec._term_ptr, 0)
         self._handle = ctypes.addressof(self._step_args)
         self._fast_step_h = nat.fast.bg_step_h
@@ -652,8 +698,10 @@ class BeerGameEnv(spaces.Env):
         self.week = None
 
     def reset(self):
-        if self._server is not None:
-            self._server.stop()  # the reset kernel rewrites the state the wave steps
+        # No request of this env is in flight (step() returns once it is answered), so the
+        # shared wave may keep serving other envs while the reset kernel rewrites this one's
+        # state; the next post publishes the new episode's arguments and the wave's acquire
+        # per request reads the reset state.
         obs = self._vec.reset()
         self.week = 0
         self._last_act = None

@@ -38,8 +38,10 @@ extern "C" {
 /* 5 (round 4): scg_sc_state.inbox_tk is uint8 [inbox_size][N] (byte-packed entries);
  *   shipment delays up to SCG_BG_MAX_DELAY = 4096; full_table of any row count.
  * 6 (round 5): the BeerGame step server (scg_bg_server_box, scg_bg_server, scg_bg_server_step,
- *   scg_bg_server_stop) and the testing hook scg_sc_nodes_max_blocks. */
-#define SCG_ABI_VERSION 6
+ *   scg_bg_server_stop) and the testing hook scg_sc_nodes_max_blocks.
+ * 7 (round 6): the step server serves up to SCG_BG_SERVER_SLOTS envs from one wave
+ *   (scg_bg_server_slot, attach / detach / post / wait), mixing-hash check word. */
+#define SCG_ABI_VERSION 7
 
 #if defined(__GNUC__)
 #define SCG_API __attribute__((visibility("default")))
@@ -241,58 +243,103 @@ SCG_API int scg_bg_step_timed(const scg_bg_config* cfg, scg_bg_state* st, const 
                               int32_t* done, void* start_event, void* stop_event, void* stream);
 
 /*
- * Step server for a few envs stepped one week per host call (the drop-in BeerGameEnv:
+ * Step server for drop-in envs stepped one week per host call (BeerGameEnv:
  * beergame_env.py:66-138 is one Python call per week). A launch plus a stream
  * synchronisation per week costs more than the reference's whole step, so instead one wave
- * stays resident: it polls a mailbox in host-mapped memory, runs the week body of
- * bg_step_kernel (the same code, the same state buffers) when scg_bg_server_step posts a
- * week's plan, and writes obs / reward to the caller's buffers (host-mapped, so the host reads
- * them at once). Up to 64 envs, variant 1, separate state buffers (no slab), no auto-reset.
+ * stays resident per server: it polls a mailbox in host-mapped memory and runs the week body
+ * of bg_step_kernel (the same code) on the state of whichever env posted a week. One server
+ * serves up to SCG_BG_SERVER_SLOTS envs (a slot each: its request line, its answer word and
+ * its kernel arguments), so a process that steps many drop-in envs in turn (a DummyVecEnv)
+ * keeps ONE resident wave and one stream per device, not one per env. Every slot's config
+ * must have the server's levels and demand mode; up to 64 envs per slot; variant 1, separate
+ * state buffers (no slab), no auto-reset.
  *
- * The wave exits on scg_bg_server_stop, or by itself after idle_us without a request, so it
- * never outlives its process; scg_bg_server_step (re)launches it when it is not running or
- * may have timed out (idle for more than idle_us / 2 on the host's clock). Work the caller
- * launches on the state (reset, other steps) must be complete before scg_bg_server_step and
- * must not start before scg_bg_server_stop returns; the mailbox must outlive the wave.
+ * The wave exits on scg_bg_server_stop, or by itself after idle_us without a request on any
+ * slot, so it never outlives its process; scg_bg_server_post (re)launches it when it is not
+ * running or may have timed out (idle for more than idle_us / 2 on the host's clock). When it
+ * starts, every slot whose request is newer than its answer is served. Work the caller
+ * launches on an env's state (reset, other steps) must be complete before that env's next
+ * post, and must not start while one of its posts is unanswered; the mailbox must outlive
+ * the wave. post/wait/step of different slots may run on different host threads.
  */
-typedef struct scg_bg_server_box {  /* host-mapped (hipHostMalloc mapped + coherent), 128 B */
-  /* the request: one 64-byte line, which the wave reads in one load */
-  uint32_t req_seq;      /* request number (a new number is a new request)                   */
-  int32_t cmd;           /* 0 step, 1 exit                                                  */
-  uint32_t wpack;        /* the week's plan, as bg_step_kernel's packed word                */
-  int32_t week;          /* the week being stepped (1..max_weeks)                           */
-  int32_t demand_fixed;  /* customer_demand[week - 1] for SCG_DEMAND_FIXED                  */
-  int32_t n_inline;      /* L when env 0's action row travels in action[] (one env, L <= 8) */
-  int32_t pad0;
-  uint32_t check;        /* 0x9E3779B9 + sum over the line's words i != 7 of word_i * (2i + 1),
-                            mod 2^32: a read of the line that mixes two requests is read again */
+#define SCG_BG_SERVER_SLOTS 15
+#define SCG_BG_SERVER_ARGS_BYTES 512
+#define SCG_PENDING 5 /* scg_bg_server_wait: not answered within spin_us (not an error) */
+
+typedef struct scg_bg_server_line { /* one 64-byte request line, read by the wave in one load */
+  uint32_t req_seq;      /* request number (a new number is a new request)                      */
+  int32_t cmd;           /* 0: step                                                            */
+  uint32_t wpack;        /* the week's plan, as bg_step_kernel's packed word                   */
+  int32_t week;          /* the week being stepped (1..max_weeks)                              */
+  int32_t demand_fixed;  /* customer_demand[week - 1] for SCG_DEMAND_FIXED                     */
+  int32_t n_inline;      /* L when env 0's action row travels in action[] (one env, L <= 8)    */
+  uint32_t gen;          /* generation of the slot's kernel arguments (args[slot] below)       */
+  uint32_t check;        /* scg mixing hash of the line's other 15 words: a read of the line
+                            that mixes two requests is read again                            */
   int32_t action[8];
-  /* the answer, on its own line */
-  uint32_t done_seq;     /* last request served                                             */
-  uint32_t exit_seq;     /* last request seen when the wave exited                          */
-  int32_t pad1[14];
+} scg_bg_server_line;
+
+typedef struct scg_bg_server_box { /* host-mapped (hipHostMalloc mapped + coherent) */
+  scg_bg_server_line req[SCG_BG_SERVER_SLOTS + 1]; /* slot k's request line is req[k]       */
+  uint32_t done_seq[16];  /* slot k's last request served (written by the wave)             */
+  uint32_t n_slots;       /* the wave polls slots 0 .. n_slots - 1                          */
+  uint32_t exit_req;      /* the wave exits when this differs from its launch value         */
+  uint32_t exit_seq;      /* written by the wave as it exits: the exit_req it saw last     */
+  uint32_t pad[13];
+  unsigned char args[SCG_BG_SERVER_SLOTS][SCG_BG_SERVER_ARGS_BYTES]; /* opaque, per slot    */
 } scg_bg_server_box;
 
 typedef struct scg_bg_server {
-  scg_bg_server_box* box_host;  /* the mailbox's host address                             */
-  scg_bg_server_box* box_dev;   /* its device address (hipHostGetDevicePointer)           */
-  const int32_t* action;        /* DEVICE-visible int32 [N][L], read each request         */
-  const int32_t* action_host;   /* its host address, or NULL: with one env of L <= 8, the
-                                   row is copied into the request line (no second read)  */
-  int32_t* obs;                 /* DEVICE-visible int32 [N][L]                            */
-  int32_t* reward;              /* DEVICE-visible int32 [N]                               */
-  void* stream;                 /* the wave's stream: a non-blocking one of the caller's  */
-  int32_t idle_us;              /* the wave exits after this long without a request       */
-  int32_t running;              /* out: the wave may be running                           */
-  int64_t last_ns;              /* out: host monotonic time of the last request served    */
-  int64_t launches;             /* out: waves launched so far                             */
+  scg_bg_server_box* box_host; /* the mailbox's host address                                */
+  scg_bg_server_box* box_dev;  /* its device address (hipHostGetDevicePointer)              */
+  void* stream;                /* the wave's stream: a non-blocking one of the caller's (a
+                                  high-priority one keeps the parked wave off the hardware
+                                  queues of normal-priority streams)                         */
+  int32_t levels;              /* the wave's instantiation: every slot's config must match  */
+  int32_t demand_mode;
+  int32_t idle_us;             /* the wave exits after this long without a request          */
+  int32_t check_us;            /* a waiting step checks this often whether the wave has
+                                  gone (0: 2 s)                                              */
+  /* host bookkeeping: zero before first use */
+  int32_t lock;
+  int32_t running;             /* the wave may be running                                   */
+  uint32_t slots_used;         /* bit k: slot k attached                                    */
+  int32_t pad;
+  int64_t last_ns;             /* host monotonic time of the last request posted or served  */
+  int64_t launches;            /* waves launched so far                                     */
 } scg_bg_server;
 
-/* step(action) for the st->n_envs <= 64 envs through the server wave; *done as scg_bg_step. */
-SCG_API int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server* sv, int32_t* done);
+typedef struct scg_bg_server_slot {
+  scg_bg_server* server;       /* set by scg_bg_server_attach                               */
+  const int32_t* action;       /* DEVICE-visible int32 [N][L], read each request            */
+  const int32_t* action_host;  /* its host address, or NULL: with one env of L <= 8 the row
+                                  is copied into the request line (no second read)         */
+  int32_t* obs;                /* DEVICE-visible int32 [N][L]                               */
+  int32_t* reward;             /* DEVICE-visible int32 [N]                                  */
+  int32_t index;               /* out: the slot, -1 when detached                           */
+  uint32_t gen;                /* out: generation of the arguments last published           */
+  uint32_t seq;                /* out: the request last posted                              */
+  int32_t week;                /* out: the week it steps                                    */
+  int32_t done;                /* out: that week is the terminal one                        */
+  int32_t relaunches;          /* out: waves this slot's waits launched again (wave gone)   */
+} scg_bg_server_slot;
 
-/* Ask the server wave to exit and wait for it (a no-op when it is not running). */
+/* Take a free slot of `sv` for one env (slot->action/obs/reward set by the caller). */
+SCG_API int scg_bg_server_attach(scg_bg_server* sv, scg_bg_server_slot* slot);
+/* Give the slot back (no request of it may be unanswered). */
+SCG_API int scg_bg_server_detach(scg_bg_server_slot* slot);
+/* Post step(action) for the st->n_envs <= 64 envs of the slot; launches the wave if needed. */
+SCG_API int scg_bg_server_post(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server_slot* slot);
+/* Wait for the slot's posted step: SCG_OK (st->week advanced, *done as scg_bg_step),
+ * SCG_PENDING after spin_us (< 0: no limit; the wait then fails after 60 s), or an error
+ * (a HIP error of the wave's stream at once; a wave gone twice without answering). */
+SCG_API int scg_bg_server_wait(scg_bg_state* st, scg_bg_server_slot* slot, int64_t spin_us, int32_t* done);
+/* post + wait without limit. */
+SCG_API int scg_bg_server_step(const scg_bg_config* cfg, scg_bg_state* st, scg_bg_server_slot* slot, int32_t* done);
+/* Ask the wave to exit and wait for it (a no-op when it is not running). */
 SCG_API int scg_bg_server_stop(scg_bg_server* sv);
+/* The request line's check word (the mixing hash the wave recomputes). */
+SCG_API uint32_t scg_bg_server_line_check(const scg_bg_server_line* line);
 
 /*
  * K consecutive steps in one launch per <= SCG_BG_ROLLOUT_MAX weeks, state held in

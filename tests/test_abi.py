@@ -148,10 +148,12 @@ def test_step_rejects_shards_beyond_int32_before_any_launch():
 
 
 def test_step_server_validates_before_any_launch():
-    """scg_bg_server_step / scg_bg_server_stop: every argument the resident wave depends on is
-    checked on the host before anything is launched (more than 64 envs, BeerGameEnv2, the slab
-    layout, a missing mailbox or buffer, the null stream, an idle time-out out of range, a step
-    before reset or past the horizon); stopping a server that never ran is a no-op."""
+    """scg_bg_server_attach / _post / _detach / _stop: every argument the resident wave depends
+    on is checked on the host before anything is launched (a slot without buffers, the null
+    stream, levels or an idle time-out out of range, all slots taken; more than 64 envs, a
+    config that is not the server's, BeerGameEnv2, the slab layout, a step before reset or past
+    the horizon, a detached slot); attach and detach keep the polled slot count; stopping a
+    server that never ran is a no-op."""
     from gym_supplychain_amd import _native as nat
     T = 35
     c = nat.BgConfig()
@@ -168,39 +170,96 @@ def test_step_server_validates_before_any_launch():
     st.n_envs, st.env_offset, st.week = 1, 0, 0
     for f in ("inventory", "backlog", "orders_placed", "shipments"):
         setattr(st, f, fake)
-    box = nat.BgServerBox()
-    sv = nat.BgServer(ctypes.addressof(box), fake, fake, None, fake, fake, fake, 20000, 0, 0, 0)
+    box = nat.BgServerBox()  # ordinary host memory: attach/detach only write the mailbox
+    sv = nat.BgServer(ctypes.addressof(box), fake, fake, 4, nat.SCG_DEMAND_FIXED, 20000, 0)
     done = ctypes.c_int32(0)
 
-    def step(expect, text):
-        rc = nat.lib.scg_bg_server_step(ctypes.byref(c), ctypes.byref(st), ctypes.byref(sv), ctypes.byref(done))
+    def attach(slot, expect=0, text=""):
+        rc = nat.lib.scg_bg_server_attach(ctypes.byref(sv), ctypes.byref(slot))
+        assert rc == expect and text in (nat.last_error() if rc else ""), (rc, nat.last_error())
+
+    slot = nat.BgServerSlot(None, fake, None, None, fake, -1)
+    attach(slot, nat.SCG_ERR_INVALID, "required")
+    slot.obs = fake
+    sv.stream = None
+    attach(slot, nat.SCG_ERR_INVALID, "null stream")
+    sv.stream = fake
+    sv.idle_us = 10
+    attach(slot, nat.SCG_ERR_INVALID, "idle_us")
+    sv.idle_us = 20000
+    sv.levels = 17
+    attach(slot, nat.SCG_ERR_INVALID, "levels")
+    sv.levels = 4
+    slots = [nat.BgServerSlot(None, fake, None, fake, fake, -1) for _ in range(nat.BG_SERVER_SLOTS)]
+    for k, s in enumerate(slots):
+        attach(s)
+        assert s.index == k and box.n_slots == k + 1
+    attach(slot, nat.SCG_ERR_INVALID, "slots are taken")
+    for k in (3, nat.BG_SERVER_SLOTS - 1):
+        assert nat.lib.scg_bg_server_detach(ctypes.byref(slots[k])) == 0 and slots[k].index == -1
+    assert box.n_slots == nat.BG_SERVER_SLOTS - 1 and sv.slots_used == (1 << nat.BG_SERVER_SLOTS) - 1 - 8 - (1 << 14)
+    attach(slot)
+    assert slot.index == 3  # the lowest free slot
+    slot = slots[0]
+
+    def post(expect, text):
+        rc = nat.lib.scg_bg_server_post(ctypes.byref(c), ctypes.byref(st), ctypes.byref(slot))
         assert rc == expect and text in nat.last_error(), (rc, nat.last_error())
 
     st.n_envs = 65
-    step(nat.SCG_ERR_INVALID, "64")
+    post(nat.SCG_ERR_INVALID, "64")
     st.n_envs = 1
-    sv.obs = None
-    step(nat.SCG_ERR_INVALID, "required")
-    sv.obs = fake
-    sv.stream = None
-    step(nat.SCG_ERR_INVALID, "null stream")
-    sv.stream = fake
-    sv.idle_us = 10
-    step(nat.SCG_ERR_INVALID, "idle_us")
-    sv.idle_us = 20000
     st.slab = fake
-    step(nat.SCG_ERR_INVALID, "slab")
+    post(nat.SCG_ERR_INVALID, "slab")
     st.slab = None
     st.week = -1
-    step(nat.SCG_ERR_NOT_RESET, "reset")
+    post(nat.SCG_ERR_NOT_RESET, "reset")
     st.week = T
-    step(nat.SCG_ERR_PAST_HORIZON, "terminal")
-    c.variant = 2
+    post(nat.SCG_ERR_PAST_HORIZON, "terminal")
     st.week = 0
-    step(nat.SCG_ERR_INVALID, "variant 1")
-    assert sv.running == 0 and sv.launches == 0 and box.req_seq == 0  # nothing was posted or launched
+    c.demand_mode = nat.SCG_DEMAND_UNIFORM
+    c.demand_lo, c.demand_hi = 0, 8
+    post(nat.SCG_ERR_INVALID, "not the server's")
+    c.demand_mode = nat.SCG_DEMAND_FIXED
+    c.variant = 2
+    post(nat.SCG_ERR_INVALID, "variant 1")
+    c.variant = 1
+    assert nat.lib.scg_bg_server_detach(ctypes.byref(slot)) == 0
+    post(nat.SCG_ERR_INVALID, "not attached")
+    rc = nat.lib.scg_bg_server_wait(ctypes.byref(st), ctypes.byref(slot), 0, ctypes.byref(done))
+    assert rc == nat.SCG_ERR_INVALID
+    # nothing was posted or launched
+    assert sv.running == 0 and sv.launches == 0 and all(box.req[k].req_seq == 0 for k in range(16))
     assert nat.lib.scg_bg_server_stop(ctypes.byref(sv)) == 0
     assert nat.lib.scg_bg_server_stop(None) == nat.SCG_ERR_INVALID
+
+
+def test_step_server_check_word_mixes_every_word():
+    """The request line's check (scg_bg_server_line_check, recomputed by the wave) is a mixing
+    hash: a read that mixes two requests is caught even when two action words move by amounts
+    a weighted sum would cancel (+19k in word 8, -17k in word 9), and when any single word
+    changes."""
+    from gym_supplychain_amd import _native as nat
+    rng = np.random.default_rng(0)
+    line = nat.BgServerLine()
+    for k in range(200):
+        words = rng.integers(0, 2 ** 32, 16, dtype=np.uint64)
+        ctypes.memmove(ctypes.addressof(line), words.astype(np.uint32).tobytes(), 64)
+        h = nat.lib.scg_bg_server_line_check(ctypes.byref(line))
+        w2 = words.astype(np.uint32).copy()
+        w2[8] = np.uint32((int(w2[8]) + 19 * (k + 1)) % 2 ** 32)
+        w2[9] = np.uint32((int(w2[9]) - 17 * (k + 1)) % 2 ** 32)
+        ctypes.memmove(ctypes.addressof(line), w2.tobytes(), 64)
+        assert nat.lib.scg_bg_server_line_check(ctypes.byref(line)) != h
+        for i in (0, 1, 2, 3, 4, 5, 6, 8 + k % 8):
+            w3 = words.astype(np.uint32).copy()
+            w3[i] ^= np.uint32(1 << (k % 32))
+            ctypes.memmove(ctypes.addressof(line), w3.tobytes(), 64)
+            assert nat.lib.scg_bg_server_line_check(ctypes.byref(line)) != h
+        w4 = words.astype(np.uint32).copy()
+        w4[7] ^= np.uint32(0xFFFFFFFF)  # the check word itself is not hashed
+        ctypes.memmove(ctypes.addressof(line), w4.tobytes(), 64)
+        assert nat.lib.scg_bg_server_line_check(ctypes.byref(line)) == h
 
 
 def test_uniform_ints_rejects_env_ids_and_sizes_before_any_launch():

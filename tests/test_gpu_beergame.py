@@ -124,45 +124,6 @@ def test_single_env_facade(name):
             env.step(g["actions"][0, n])
 
 
-@pytest.mark.parametrize("levels", [4, 10])
-def test_step_server_matches_launch_path(levels, monkeypatch):
-    """The drop-in env's step server (one resident wave polling a host-mapped mailbox,
-    scg_bg_server_step) against the launch path (SCG_BG_SERVER=0), week for week: observation,
-    reward, done and the state rows, over three episodes (reset() stops the wave), an idle
-    time-out mid-episode (the wave exits by itself and is launched again), and L = 10 > 8 (the
-    action row read from host-mapped memory instead of travelling in the request line)."""
-    import time
-    from gym_supplychain_amd import BeerGameEnv
-    T = 30
-    rng = np.random.RandomState(levels)
-    info = dict(levels=levels, initial_inventory=[12] * levels, customer_demand=rng.randint(0, 12, T).tolist(),
-                shipment_delays=rng.randint(0, 4, T).tolist())
-    monkeypatch.setenv("SCG_BG_SERVER", "1")
-    srv = BeerGameEnv(info)
-    monkeypatch.setenv("SCG_BG_SERVER", "0")
-    ref = BeerGameEnv(info)
-    assert srv._server is not None and ref._server is None
-    for ep in range(3):
-        assert np.array_equal(srv.reset(), ref.reset())
-        for w in range(T):
-            a = rng.randint(-3, 15, levels)
-            if ep == 1 and w == 10:
-                time.sleep(3 * srv._server.IDLE_US * 1e-6)  # the wave times out and exits
-            o1, r1, d1, _ = srv.step(a)
-            o2, r2, d2, _ = ref.step(a)
-            assert np.array_equal(o1, o2) and r1 == r2 and d1 == d2, (ep, w)
-            assert srv.week == ref.week == w + 1
-        for attr in ("inventory", "backlog", "orders_placed", "inventory_costs", "backlog_costs", "all_orders_placed",
-                     "shipments"):
-            assert np.array_equal(getattr(srv, attr), getattr(ref, attr)), (ep, attr)
-        with pytest.raises(IndexError):
-            srv.step(np.zeros(levels, dtype=np.int64))
-    assert srv._server.sv.launches >= 4  # one per episode, one more after the time-out
-    srv.close()
-    srv.close()  # idempotent
-    ref.close()
-
-
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("slab", [True, False])
 def test_vec_full_table_matches_reference(name, slab):

@@ -10,7 +10,9 @@ of the reference step() on one host core.
   which writes observation, reward and the overflow word to host-mapped memory; beside it the
   launch path (SCG_BG_SERVER=0: one step-kernel launch and one stream synchronisation per
   call) and the round-4 design (pinned H2D copy, launch, two D2H copies, synchronise), on the
-  same box. The server's wave launches are counted (one per episode: reset() stops it).
+  same box. The server's wave launches are counted. And 8 envs stepped round-robin (an SB3
+  DummyVecEnv of drop-in envs): every env holds a slot of the one shared server, so the 8
+  share one resident wave; per step() call, on the server and on the launch path.
 * SupplyChain2perStageEnv.step (supplychain_env.py:703-748; reference ~136 us per step):
   the same host-mapped path, host RandomState episode draws (the reference's), float64 obs.
 * cpu: oracle.beergame.BeerGameOracle.step and oracle.supplychain.SupplyChainOracle.step
@@ -62,6 +64,39 @@ def beergame(episodes, server=True):
     if server:
         st["server_wave_launches"] = int(env._server.sv.launches)
     env.close()
+    return st
+
+
+def beergame_many(episodes, n_envs=8, server=True):
+    import numpy as np
+    os.environ["SCG_BG_SERVER"] = "1" if server else "0"
+    import gym_supplychain_amd as gsa
+    envs = [gsa.make("beergame-v0") for _ in range(n_envs)]
+    rng = np.random.RandomState(0)
+    acts = [rng.randint(0, 9, size=4) for _ in range(35 * 8)]
+    pc = time.perf_counter
+
+    def run(eps):
+        ts = []
+        for e in range(eps):
+            for env in envs:
+                env.reset()
+            for w in range(35):
+                a = acts[(e * 35 + w) % len(acts)]
+                for env in envs:
+                    t0 = pc()
+                    env.step(a)
+                    ts.append(pc() - t0)
+        return ts
+    run(2)
+    l0 = envs[0]._server.sv.launches if server else 0
+    st = _stats(run(episodes))
+    st["n_envs"] = n_envs
+    if server:
+        st["servers"] = len({id(e._server.server) for e in envs})
+        st["server_wave_launches"] = int(envs[0]._server.sv.launches - l0)
+    for env in envs:
+        env.close()
     return st
 
 
@@ -166,6 +201,10 @@ def main():
     emit("BeerGameEnv.step (step server: resident wave, host-mapped mailbox and io)", 12.8, beergame(a.bg_episodes))
     emit("BeerGameEnv.step, launch path (SCG_BG_SERVER=0: host-mapped io, one launch + stream sync)", 12.8,
          beergame(a.bg_episodes, server=False))
+    emit("BeerGameEnv.step, 8 envs round-robin (one shared step-server wave)", 12.8,
+         beergame_many(max(a.bg_episodes // 8, 4)))
+    emit("BeerGameEnv.step, 8 envs round-robin, launch path (SCG_BG_SERVER=0)", 12.8,
+         beergame_many(max(a.bg_episodes // 8, 4), server=False))
     emit("BeerGameEnv.step, round-4 design (H2D copy, launch, 2 D2H copies, sync)", 12.8, beergame_copies(a.bg_episodes))
     st, kernel = supplychain(a.sc_episodes)
     emit("SupplyChain2perStageEnv.step (host-mapped io, one launch + stream sync)", 136.0, st, kernel=kernel)
