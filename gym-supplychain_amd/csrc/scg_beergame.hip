@@ -434,18 +434,6 @@ static_assert(sizeof(scg_bg_server_box) == 17 * 64 + 64 + SCG_BG_SERVER_SLOTS * 
 static_assert(offsetof(scg_bg_server_box, done_seq) == 16 * 64 && offsetof(scg_bg_server_box, args) == 18 * 64,
               "mailbox lines");
 static_assert(sizeof(scg_bg_server) == 72 && sizeof(scg_bg_server_slot) == 64, "server structs");
-static int64_t mono_ns() {
-  timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return static_cast<int64_t>(ts.tv_sec) * 1000000000 + ts.tv_nsec;
-}
-
-static inline void cpu_relax() {
-#if defined(__x86_64__)
-  __builtin_ia32_pause();
-#endif
-}
-
 // The server's host bookkeeping (launch, retire, slots, argument blocks) under a spin lock in
 // the struct itself: posts and waits of different slots may come from different threads.
 struct ServerLock {

@@ -30,6 +30,7 @@
 #include <cstring>
 
 #include "scg_common.h"
+#include "scg_mailbox.h"
 #include "scg_const.h"
 #include "scg_philox.h"
 #include "scgpu.h"
@@ -556,21 +557,8 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
 }
 
 // ---- step server (scg_bg_server_*: the drop-in BeerGameEnv) -------------------------------
-// A request is one 64-byte line of the mailbox (scg_bg_server_line): 16 words, word 7 a mixing
-// hash of the other 15 (multiply, xor, rotate per word), so a read that mixes two requests is
-// detected whatever the words' differences.
-__host__ __device__ inline uint32_t server_line_check(const uint32_t (&w)[16]) {
-  uint32_t h = 0x9E3779B9u;
-  for (int i = 0; i < 16; ++i) {
-    if (i == 7) continue;
-    h ^= w[i] * 0x85EBCA6Bu + static_cast<uint32_t>(i);
-    h = (h << 13) | (h >> 19);
-    h = h * 5u + 0xE6546B64u;
-  }
-  h ^= h >> 16;
-  h *= 0xC2B2AE35u;
-  return h ^ (h >> 13);
-}
+// A request is one 64-byte line of the mailbox (scg_bg_server_line, scg_mailbox.h).
+inline __host__ __device__ uint32_t server_line_check(const uint32_t (&w)[16]) { return mailbox_check(w); }
 
 constexpr int kServerBlock = 64;
 constexpr int kServerSlots = SCG_BG_SERVER_SLOTS;

@@ -115,6 +115,31 @@ static PyObject* bg_server_step(PyObject* self, PyObject* const* args, Py_ssize_
   return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
 }
 
+/* sc_server_step(cfg, state, server): one step through the SupplyChain step server, as
+ * bg_server_step (post, spin up to 200 us with the GIL, then wait without it). */
+static PyObject* sc_server_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  void* p[3];
+  if (nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "sc_server_step expects 3 arguments");
+    return NULL;
+  }
+  for (int i = 0; i < 3; ++i)
+    if (as_ptr(args[i], &p[i])) return NULL;
+  const scg_sc_config* cfg = (const scg_sc_config*)p[0];
+  scg_sc_state* st = (scg_sc_state*)p[1];
+  scg_sc_server* sv = (scg_sc_server*)p[2];
+  int32_t done = 0;
+  int rc = scg_sc_server_post(cfg, st, sv);
+  if (rc == SCG_OK) rc = scg_sc_server_wait(cfg, st, sv, 200, &done);
+  if (rc == SCG_PENDING) {
+    Py_BEGIN_ALLOW_THREADS
+    rc = scg_sc_server_wait(cfg, st, sv, -1, &done);
+    Py_END_ALLOW_THREADS
+  }
+  return PyLong_FromLong((long)((rc << 1) | (done ? 1 : 0)));
+}
+
 /* sc_step(cfg, state, action, obs, reward, terminal_obs, flags, stream) */
 static PyObject* sc_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
   (void)self;
@@ -192,6 +217,7 @@ static PyMethodDef methods[] = {
     {"bg_server_step", (PyCFunction)(void (*)(void))bg_server_step, METH_FASTCALL, "scg_bg_server_step"},
     {"bg_step_timed", (PyCFunction)(void (*)(void))bg_step_timed, METH_FASTCALL, "scg_bg_step_timed"},
     {"sc_step", (PyCFunction)(void (*)(void))sc_step, METH_FASTCALL, "scg_sc_step"},
+    {"sc_server_step", (PyCFunction)(void (*)(void))sc_server_step, METH_FASTCALL, "scg_sc_server_post + _wait"},
     {"node_barrier", (PyCFunction)(void (*)(void))node_barrier, METH_FASTCALL, "host barrier of one node's ranks"},
     {NULL, NULL, 0, NULL},
 };

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "scg_common.h"
+#include "scg_mailbox.h"
 #if defined(SCG_NODES_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
 // Diagnostic build only: every stamp (the phase boundaries NSTAMP below, and the end of each
 // section of the act and heaps phases, SCG_ACCP(ptr, k) in scg_supplychain_core.h / _nodes.h)
@@ -149,6 +150,257 @@ struct TileWalk {
 #ifndef SCG_NODES_NT
 #define SCG_NODES_NT 2
 #endif
+// One tile of 64 envs (tile * 64 ...): the step described at the top, on the kernel arguments
+// `a`, except the step's time, flags and episode, which come from `sp` (sp.t(), sp.flags(),
+// sp.episode(): the batch kernel's launch arguments, read where used as before; the step
+// server's request). lane is the thread's lane, opaque to the compiler; w the wave index.
+struct NodesLaunchStep {  // the batch kernel: the step fields of the launch arguments
+  const ScArgs& a;
+  __device__ __forceinline__ int t() const { return a.t; }
+  __device__ __forceinline__ int flags() const { return a.flags; }
+  __device__ __forceinline__ uint32_t episode() const { return a.episode; }
+};
+
+template <int MAXD, bool F64, bool LED, class Step>
+__device__ __forceinline__ void sc_nodes_tile(const ScArgs& a, int64_t tile, int lane, int w, int W, int E,
+                                              const Step& sp) {
+  using ObsT = typename std::conditional<F64, double, float>::type;
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr bool ledgers = LED;
+  // streaming stores for the heap copy-back and the observation and stock rows (SCG_NODES_NT)
+  constexpr bool kStream = SCG_NODES_NT == 2 || (SCG_NODES_NT == 1 && LED);
+  const ScCtx& c = a.c;
+  const int NN = c.n_nodes, P = c.P, NP = NN * P, H = c.H;
+  const int Ap = c.A | 1, Op = c.O | 1;  // odd row strides: lanes hit distinct banks
+  double* hval = reinterpret_cast<double*>(smem);
+  double* recv = hval + static_cast<int64_t>(NP) * H * 64;  // released sums [NP][64]
+  double* ibval = recv + NP * 64;
+  double* cost_v = ibval + static_cast<int64_t>(E) * 64;
+  double* stk = cost_v + NN * 64;  // the tile's stocks [NP][64] for the step
+  double* ret0 = stk + NP * 64;    // episode returns [64] (wave 0's prefetch)
+  ObsT* obs_t = reinterpret_cast<ObsT*>(ret0 + 64);
+  int32_t* htk = reinterpret_cast<int32_t*>(obs_t + 64 * Op);
+  int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
+  int32_t* ibtk = hsz + NP * 64;
+  int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
+  int32_t* amb = cost_k + NN * 64;
+  uint64_t* lword = reinterpret_cast<uint64_t*>(amb + W * 64);  // ledger entry marks and types [NP][64]
+  float* act_t = reinterpret_cast<float*>(lword + NP * 64);
+  const bool terminal = sp.flags() & 1;
+  const bool autoreset = sp.flags() & 2;
+  const int64_t n0 = tile * 64;
+  const int64_t n = n0 + lane;
+  const int nb = a.n - n0 < 64 ? static_cast<int>(a.n - n0) : 64;  // envs of this tile
+  const bool live = lane < nb;
+  auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
+  // heaps and sizes in HBM (the batch's base pointers, column n); stocks in the LDS copy
+  ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, sp.episode(), 0};
+  g.soff = lane;
+  g.hoff = n;
+  if (ledgers) {  // the nodes' entries to their slots (column n = base + n0 + soff), reduced below
+    g.led_v = a.ledp_v + n0;
+    g.led_stride = a.n;
+    g.led_word = lword + lane;
+    g.led_word_stride = 64;
+  }
+  NSTAMP(0);
+#if defined(SCG_NODES_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+  ScAcc acc_{};
+  g.dbg = &acc_;
+#define NACC(k) SCG_ACCP(&acc_, k)
+#else
+#define NACC(k)
+#endif
+
+  // the step's observation row, whichever buffer(s) it goes to (chosen at the copy-out)
+  ObsT* const orow = obs_t + lane * Op;
+  auto sink = [&](int o, double x) { orow[o] = static_cast<ObsT>(x); };
+  const NodesInbox in{ibtk + lane, ibval + lane, 64};
+  const float* act = act_t + lane * Ap;
+
+  // stage, one memory round: every thread requests its share of the tile's action rows
+  // (one contiguous span), every wave its node's stocks, heap sizes and the first kStage
+  // slots of each heap, wave 0 the episode returns; nothing is waited for until all are in
+  // flight. Then everything to LDS, the rest of a longer heap, and what each heap releases.
+  bool bad = false;
+  {
+    constexpr int kAct = 4;  // action elements per thread per round
+    const float* src = a.act + n0 * c.A;
+    const int na = nb * c.A;
+    float av[kAct];
+#pragma unroll
+    for (int u = 0; u < kAct; ++u)
+      if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
+    const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
+    for (int i = w; i < NN; i += W)
+      for (int p = 0; p < P; ++p) {
+        const int hp = i * P + p;
+        if (!live) continue;
+        const int64_t r = static_cast<int64_t>(hp) * a.n + n;
+        const double st = a.stock[r];
+        const int32_t sz = a.size[r];
+        stk[hp * 64 + lane] = st;
+        hsz[hp * 64 + lane] = sz;
+        const HeapView lh = lheap(hp);
+        // the heap's first slots are requested with the size (sc_nodes_copy_heap, shared
+        // with the host harness); a longer heap costs a round more
+        sc_nodes_copy_heap(HeapView{a.tk + static_cast<int64_t>(hp) * H * a.n + n,
+                                    a.val + static_cast<int64_t>(hp) * H * a.n + n, a.n},
+                           lh, H, sz);
+        bad |= !sc_recv_scan(lh, sz, sp.t(), recv[hp * 64 + lane]);
+      }
+    {
+      TileWalk tw(threadIdx.x, blockDim.x, c.A);
+#pragma unroll
+      for (int u = 0; u < kAct; ++u, tw.next())
+        if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) act_t[tw.r * Ap + tw.k] = av[u];
+      for (int q = threadIdx.x + kAct * blockDim.x; q < na; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
+    }
+    if (w == 0 && live && a.ep_ret) ret0[lane] = r0;
+  }
+  amb[w * 64 + lane] = bad ? 1 : 0;
+  NSTAMP(5);
+  __syncthreads();
+  NSTAMP(6);
+  bool flagged = (sp.flags() & 4) != 0;
+  for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
+  const bool go = live && !flagged;
+
+  // act: every node at once (a node's act needs only what its own heaps release)
+  if (go)
+    for (int i = w; i < NN; i += W) {
+      const Num cst = sc_nodes_act<MAXD, !LED>(c, g, in, recv + i * P * 64 + lane, 64, act, sp.t(), i);
+      NACC(12);
+      cost_v[i * 64 + lane] = cst.v;
+      cost_k[i * 64 + lane] = cst.k;
+      for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
+      NACC(13);
+    }
+  NSTAMP(1);
+  __syncthreads();
+  NSTAMP(2);
+
+  // heaps
+  if (go)
+    for (int i = w; i < NN; i += W) {
+      WordCache ltc{0, U4{0, 0, 0, 0}, false};
+      int a_i = 0, lt_i = 0;
+      for (int p = 0; p < P; ++p) {
+        const int hp = i * P + p;
+        sc_nodes_heap<kStream>(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, sp.t(), i, p, a_i, lt_i, sink);
+      }
+    }
+  NSTAMP(3);
+
+  // ledgers: entry q of an env, the nodes' entries added in node order (:750-760); at an
+  // auto-reset the finished episode's ledger is kept and the new one starts at int 0
+  auto ledger_put = [&](int q, double lv, int32_t lk) {
+    const int64_t at = q * a.n + n;
+    if (autoreset) {
+      if (a.led_fv) {
+        a.led_fv[at] = lv;
+        a.led_fk[at] = lk;
+      }
+      lv = 0.0;
+      lk = np_kind_abi(NK_INT);
+    }
+    a.led_v[at] = lv;
+    a.led_k[at] = lk;
+  };
+  // entries first, first + step, ... of an env, two at a time (their loads in flight together)
+  auto ledger_entries = [&](int first, int step) {
+    const int nq = 2 * SCG_SC_LEDGER_KEYS * P;
+    for (int q0 = first; q0 < nq; q0 += 2 * step) {
+      const int q1 = q0 + step < nq ? q0 + step : -1;
+      const int64_t at0 = q0 * a.n + n, at1 = (q1 >= 0 ? q1 : q0) * a.n + n;
+      double lv0 = a.led_v[at0], lv1 = a.led_v[at1];
+      int32_t lk0 = a.led_k[at0], lk1 = a.led_k[at1];
+      sc_ledger_reduce_pair(c, q0, q1, a.ledp_v + n, a.n, lword + lane, 64, lv0, lk0, lv1, lk1);
+      ledger_put(q0, lv0, lk0);
+      if (q1 >= 0) ledger_put(q1, lv1, lk1);
+    }
+  };
+#if SCG_NODES_LED_EARLY
+  // Every slot and mark of an acted env is in place since the act barrier, so each wave
+  // reduces its share of the entries as soon as its heaps are done: the slot loads overlap
+  // the other waves' heaps and wave 0's reward instead of forming a phase of their own after
+  // the last barrier. A flagged env's slots are written by wave 0's serial walk below, which
+  // then reduces that env's entries itself.
+  if (ledgers && live && !flagged) ledger_entries(w, W);
+#endif
+
+  // reward
+  if (w == 0 && live) {
+    double reward;
+    if (flagged) {  // untouched by act and heaps: the serial walk on its staged heaps
+      reward = sc_nodes_serial<MAXD, !LED>(c, g, lheap, hsz + lane, 64, in, act, sp.t(), sink);
+#if SCG_NODES_LED_EARLY
+      if (ledgers) ledger_entries(0, 1);
+#endif
+    } else {
+      Num total = pyint(0);
+      for (int i = 0; i < NN; ++i) total = np_add(total, Num{cost_v[i * 64 + lane], cost_k[i * 64 + lane]});
+      reward = np_neg(total).v;
+    }
+    a.rew[n] = reward;
+    if (a.ep_ret) {
+      const double r = ret0[lane] + reward;  // episode_rewards += current_reward (:739)
+      if (terminal && a.final_ret) a.final_ret[n] = r;
+      a.ep_ret[n] = autoreset ? 0.0 : r;
+    }
+    for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, sp.t(), k, sink);  // (:771)
+    sc_observe_tail(c, sp.t(), sink);                                               // (:786)
+  }
+  __syncthreads();
+  NSTAMP(7);
+
+#if !SCG_NODES_LED_EARLY
+  if (ledgers && live) ledger_entries(w, W);
+#endif
+
+  // out: the tile is this step's observation — obs, or the terminal observation when the
+  // env resets now (then wave 0 writes the reset observation to obs), or both
+  ObsT* const dst0 = static_cast<ObsT*>(autoreset ? a.term_obs : a.obs);
+  ObsT* const dst1 = (terminal && !autoreset) ? static_cast<ObsT*>(a.term_obs) : nullptr;
+  TileWalk tw(threadIdx.x, blockDim.x, c.O);
+  for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
+    const ObsT x = obs_t[tw.r * Op + tw.k];
+    if constexpr (kStream) {
+      if (dst0) __builtin_nontemporal_store(x, &dst0[n0 * c.O + q]);
+      if (dst1) __builtin_nontemporal_store(x, &dst1[n0 * c.O + q]);
+    } else {
+      if (dst0) dst0[n0 * c.O + q] = x;
+      if (dst1) dst1[n0 * c.O + q] = x;
+    }
+  }
+  if (autoreset) {  // after the barrier every wave's heap copy-back has landed
+    if (w == 0 && live) {
+      g.episode = sp.episode() + 1;
+      g.led_v = nullptr;   // the ledger was restarted above
+      sc_reset_env(c, g);  // heaps in HBM, stocks in the LDS copy
+      ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
+      sc_observe(c, g, 0, out);
+    }
+    __syncthreads();
+  }
+  if (live) {  // the stocks of this wave's nodes back, one 64-env row per instruction (the
+               // next tile's stage rewrites these rows: the same wave)
+    for (int i = w; i < NN; i += W)
+      for (int p = 0; p < P; ++p) {
+        if constexpr (kStream)
+          __builtin_nontemporal_store(stk[(i * P + p) * 64 + lane], &a.stock[(i * P + p) * a.n + n]);
+        else
+          a.stock[(i * P + p) * a.n + n] = stk[(i * P + p) * 64 + lane];
+      }
+    if (g.overflow) atomicOr(a.err, 1);
+  }
+  NSTAMP(4);
+#undef NACC
+  // the next tile's stage rewrites the action tile, ret0 and, per wave, only the stock, size
+  // and heap rows of its own nodes (whose stocks it copied back just above); the rows other
+  // waves read (the observation tile) are next written after that tile's first barrier
+}
+
 // Four waves per SIMD (<= 128 VGPRs): two blocks of eight waves per CU, which is also what
 // their LDS allows.
 // F64: float64 observations; LED: build_info ledgers (a separate instantiation, so the
@@ -159,15 +411,9 @@ struct TileWalk {
 template <int MAXD, bool F64, bool LED>
 __global__ __launch_bounds__(64 * kNodesMaxWaves) __attribute__((amdgpu_waves_per_eu(SCG_NODES_WPE)))
 void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
-  using ObsT = typename std::conditional<F64, double, float>::type;
-  extern __shared__ __align__(16) unsigned char smem[];
   // the wave index is wave-uniform: said so, node records are read with scalar loads
   const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_tiles = (a_arg.n + 63) / 64;
-  constexpr bool ledgers = LED;
-  // streaming stores for the heap copy-back and the observation and stock rows (SCG_NODES_NT)
-  constexpr bool kStream = SCG_NODES_NT == 2 || (SCG_NODES_NT == 1 && LED);
-
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     // the lane index, opaque to the compiler inside each tile: the per-lane LDS and HBM
     // addresses derived from it are computed where used, not hoisted out of the tile loop
@@ -181,237 +427,77 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
     KArgPtr ap = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(ap));
     const ScArgs& a = *(const ScArgs*)ap;
-    const ScCtx& c = a.c;
-    const int NN = c.n_nodes, P = c.P, NP = NN * P, H = c.H;
-    const int Ap = c.A | 1, Op = c.O | 1;  // odd row strides: lanes hit distinct banks
-    double* hval = reinterpret_cast<double*>(smem);
-    double* recv = hval + static_cast<int64_t>(NP) * H * 64;  // released sums [NP][64]
-    double* ibval = recv + NP * 64;
-    double* cost_v = ibval + static_cast<int64_t>(E) * 64;
-    double* stk = cost_v + NN * 64;  // the tile's stocks [NP][64] for the step
-    double* ret0 = stk + NP * 64;    // episode returns [64] (wave 0's prefetch)
-    ObsT* obs_t = reinterpret_cast<ObsT*>(ret0 + 64);
-    int32_t* htk = reinterpret_cast<int32_t*>(obs_t + 64 * Op);
-    int32_t* hsz = htk + static_cast<int64_t>(NP) * H * 64;
-    int32_t* ibtk = hsz + NP * 64;
-    int32_t* cost_k = ibtk + static_cast<int64_t>(E) * 64;
-    int32_t* amb = cost_k + NN * 64;
-    uint64_t* lword = reinterpret_cast<uint64_t*>(amb + W * 64);  // ledger entry marks and types [NP][64]
-    float* act_t = reinterpret_cast<float*>(lword + NP * 64);
-    const bool terminal = a.flags & 1;
-    const bool autoreset = a.flags & 2;
-    const int64_t n0 = tile * 64;
-    const int64_t n = n0 + lane;
-    const int nb = a.n - n0 < 64 ? static_cast<int>(a.n - n0) : 64;  // envs of this tile
-    const bool live = lane < nb;
-    auto lheap = [&](int hp) { return HeapView{htk + hp * H * 64 + lane, hval + hp * H * 64 + lane, 64}; };
-    // heaps and sizes in HBM (the batch's base pointers, column n); stocks in the LDS copy
-    ScEnv g{stk, a.tk, a.val, a.size, 64, a.n, static_cast<uint32_t>(a.env_offset + n), n, a.episode, 0};
-    g.soff = lane;
-    g.hoff = n;
-    if (ledgers) {  // the nodes' entries to their slots (column n = base + n0 + soff), reduced below
-      g.led_v = a.ledp_v + n0;
-      g.led_stride = a.n;
-      g.led_word = lword + lane;
-      g.led_word_stride = 64;
-    }
-    NSTAMP(0);
-#if defined(SCG_NODES_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
-    ScAcc acc_{};
-    g.dbg = &acc_;
-#define NACC(k) SCG_ACCP(&acc_, k)
-#else
-#define NACC(k)
-#endif
-
-    // the step's observation row, whichever buffer(s) it goes to (chosen at the copy-out)
-    ObsT* const orow = obs_t + lane * Op;
-    auto sink = [&](int o, double x) { orow[o] = static_cast<ObsT>(x); };
-    const NodesInbox in{ibtk + lane, ibval + lane, 64};
-    const float* act = act_t + lane * Ap;
-
-    // stage, one memory round: every thread requests its share of the tile's action rows
-    // (one contiguous span), every wave its node's stocks, heap sizes and the first kStage
-    // slots of each heap, wave 0 the episode returns; nothing is waited for until all are in
-    // flight. Then everything to LDS, the rest of a longer heap, and what each heap releases.
-    bool bad = false;
-    {
-      constexpr int kAct = 4;  // action elements per thread per round
-      const float* src = a.act + n0 * c.A;
-      const int na = nb * c.A;
-      float av[kAct];
-#pragma unroll
-      for (int u = 0; u < kAct; ++u)
-        if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
-      const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
-      for (int i = w; i < NN; i += W)
-        for (int p = 0; p < P; ++p) {
-          const int hp = i * P + p;
-          if (!live) continue;
-          const int64_t r = static_cast<int64_t>(hp) * a.n + n;
-          const double st = a.stock[r];
-          const int32_t sz = a.size[r];
-          stk[hp * 64 + lane] = st;
-          hsz[hp * 64 + lane] = sz;
-          const HeapView lh = lheap(hp);
-          // the heap's first slots are requested with the size (sc_nodes_copy_heap, shared
-          // with the host harness); a longer heap costs a round more
-          sc_nodes_copy_heap(HeapView{a.tk + static_cast<int64_t>(hp) * H * a.n + n,
-                                      a.val + static_cast<int64_t>(hp) * H * a.n + n, a.n},
-                             lh, H, sz);
-          bad |= !sc_recv_scan(lh, sz, a.t, recv[hp * 64 + lane]);
-        }
-      {
-        TileWalk tw(threadIdx.x, blockDim.x, c.A);
-#pragma unroll
-        for (int u = 0; u < kAct; ++u, tw.next())
-          if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) act_t[tw.r * Ap + tw.k] = av[u];
-        for (int q = threadIdx.x + kAct * blockDim.x; q < na; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
-      }
-      if (w == 0 && live && a.ep_ret) ret0[lane] = r0;
-    }
-    amb[w * 64 + lane] = bad ? 1 : 0;
-    NSTAMP(5);
-    __syncthreads();
-    NSTAMP(6);
-    bool flagged = (a.flags & 4) != 0;
-    for (int v = 0; v < W; ++v) flagged |= amb[v * 64 + lane] != 0;
-    const bool go = live && !flagged;
-
-    // act: every node at once (a node's act needs only what its own heaps release)
-    if (go)
-      for (int i = w; i < NN; i += W) {
-        const Num cst = sc_nodes_act<MAXD, !LED>(c, g, in, recv + i * P * 64 + lane, 64, act, a.t, i);
-        NACC(12);
-        cost_v[i * 64 + lane] = cst.v;
-        cost_k[i * 64 + lane] = cst.k;
-        for (int p = 0; p < P; ++p) sc_observe_stock(c, g, i, p, sink);
-        NACC(13);
-      }
-    NSTAMP(1);
-    __syncthreads();
-    NSTAMP(2);
-
-    // heaps
-    if (go)
-      for (int i = w; i < NN; i += W) {
-        WordCache ltc{0, U4{0, 0, 0, 0}, false};
-        int a_i = 0, lt_i = 0;
-        for (int p = 0; p < P; ++p) {
-          const int hp = i * P + p;
-          sc_nodes_heap<kStream>(c, g, lheap(hp), hsz[hp * 64 + lane], in, ltc, act, a.t, i, p, a_i, lt_i, sink);
-        }
-      }
-    NSTAMP(3);
-
-    // ledgers: entry q of an env, the nodes' entries added in node order (:750-760); at an
-    // auto-reset the finished episode's ledger is kept and the new one starts at int 0
-    auto ledger_put = [&](int q, double lv, int32_t lk) {
-      const int64_t at = q * a.n + n;
-      if (autoreset) {
-        if (a.led_fv) {
-          a.led_fv[at] = lv;
-          a.led_fk[at] = lk;
-        }
-        lv = 0.0;
-        lk = np_kind_abi(NK_INT);
-      }
-      a.led_v[at] = lv;
-      a.led_k[at] = lk;
-    };
-    // entries first, first + step, ... of an env, two at a time (their loads in flight together)
-    auto ledger_entries = [&](int first, int step) {
-      const int nq = 2 * SCG_SC_LEDGER_KEYS * P;
-      for (int q0 = first; q0 < nq; q0 += 2 * step) {
-        const int q1 = q0 + step < nq ? q0 + step : -1;
-        const int64_t at0 = q0 * a.n + n, at1 = (q1 >= 0 ? q1 : q0) * a.n + n;
-        double lv0 = a.led_v[at0], lv1 = a.led_v[at1];
-        int32_t lk0 = a.led_k[at0], lk1 = a.led_k[at1];
-        sc_ledger_reduce_pair(c, q0, q1, a.ledp_v + n, a.n, lword + lane, 64, lv0, lk0, lv1, lk1);
-        ledger_put(q0, lv0, lk0);
-        if (q1 >= 0) ledger_put(q1, lv1, lk1);
-      }
-    };
-#if SCG_NODES_LED_EARLY
-    // Every slot and mark of an acted env is in place since the act barrier, so each wave
-    // reduces its share of the entries as soon as its heaps are done: the slot loads overlap
-    // the other waves' heaps and wave 0's reward instead of forming a phase of their own after
-    // the last barrier. A flagged env's slots are written by wave 0's serial walk below, which
-    // then reduces that env's entries itself.
-    if (ledgers && live && !flagged) ledger_entries(w, W);
-#endif
-
-    // reward
-    if (w == 0 && live) {
-      double reward;
-      if (flagged) {  // untouched by act and heaps: the serial walk on its staged heaps
-        reward = sc_nodes_serial<MAXD, !LED>(c, g, lheap, hsz + lane, 64, in, act, a.t, sink);
-#if SCG_NODES_LED_EARLY
-        if (ledgers) ledger_entries(0, 1);
-#endif
-      } else {
-        Num total = pyint(0);
-        for (int i = 0; i < NN; ++i) total = np_add(total, Num{cost_v[i * 64 + lane], cost_k[i * 64 + lane]});
-        reward = np_neg(total).v;
-      }
-      a.rew[n] = reward;
-      if (a.ep_ret) {
-        const double r = ret0[lane] + reward;  // episode_rewards += current_reward (:739)
-        if (terminal && a.final_ret) a.final_ret[n] = r;
-        a.ep_ret[n] = autoreset ? 0.0 : r;
-      }
-      for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, a.t, k, sink);  // (:771)
-      sc_observe_tail(c, a.t, sink);                                               // (:786)
-    }
-    __syncthreads();
-    NSTAMP(7);
-
-#if !SCG_NODES_LED_EARLY
-    if (ledgers && live) ledger_entries(w, W);
-#endif
-
-    // out: the tile is this step's observation — obs, or the terminal observation when the
-    // env resets now (then wave 0 writes the reset observation to obs), or both
-    ObsT* const dst0 = static_cast<ObsT*>(autoreset ? a.term_obs : a.obs);
-    ObsT* const dst1 = (terminal && !autoreset) ? static_cast<ObsT*>(a.term_obs) : nullptr;
-    TileWalk tw(threadIdx.x, blockDim.x, c.O);
-    for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
-      const ObsT x = obs_t[tw.r * Op + tw.k];
-      if constexpr (kStream) {
-        if (dst0) __builtin_nontemporal_store(x, &dst0[n0 * c.O + q]);
-        if (dst1) __builtin_nontemporal_store(x, &dst1[n0 * c.O + q]);
-      } else {
-        if (dst0) dst0[n0 * c.O + q] = x;
-        if (dst1) dst1[n0 * c.O + q] = x;
-      }
-    }
-    if (autoreset) {  // after the barrier every wave's heap copy-back has landed
-      if (w == 0 && live) {
-        g.episode = a.episode + 1;
-        g.led_v = nullptr;   // the ledger was restarted above
-        sc_reset_env(c, g);  // heaps in HBM, stocks in the LDS copy
-        ObsRow out{a.obs, n * c.O, F64 ? 1 : 0};
-        sc_observe(c, g, 0, out);
-      }
-      __syncthreads();
-    }
-    if (live) {  // the stocks of this wave's nodes back, one 64-env row per instruction (the
-                 // next tile's stage rewrites these rows: the same wave)
-      for (int i = w; i < NN; i += W)
-        for (int p = 0; p < P; ++p) {
-          if constexpr (kStream)
-            __builtin_nontemporal_store(stk[(i * P + p) * 64 + lane], &a.stock[(i * P + p) * a.n + n]);
-          else
-            a.stock[(i * P + p) * a.n + n] = stk[(i * P + p) * 64 + lane];
-        }
-      if (g.overflow) atomicOr(a.err, 1);
-    }
-    NSTAMP(4);
-#undef NACC
-    // the next tile's stage rewrites the action tile, ret0 and, per wave, only the stock, size
-    // and heap rows of its own nodes (whose stocks it copied back just above); the rows other
-    // waves read (the observation tile) are next written after that tile's first barrier
+    sc_nodes_tile<MAXD, F64, LED>(a, tile, lane, w, W, E, NodesLaunchStep{a});
   }
+}
+
+// ---- step server for the drop-in SupplyChainEnv (include/scgpu.h scg_sc_server_*) --------
+// One block of the batch kernel's shape, resident: wave 0 polls the mailbox's request line
+// (lanes 0-15, system scope, with the exit word) and puts what it found in LDS; after a
+// barrier every wave either exits, sleeps and polls again, or runs tile 0 of the step with
+// the request's time, flags and episode (NodesServerStep) — the batch kernel's code — and
+// then lane 0 publishes the request number with a system-scope release store. At launch the
+// last request served is the answer word, so a request posted while no block ran is served
+// first. It exits when exit_req changes or after idle_ticks of the 100 MHz real-time clock
+// without a request, and writes the exit word it saw as it goes.
+__shared__ int32_t s_srv_req[4];  // t, flags, episode, command (0 none, 1 step, 2 exit)
+struct NodesServerStep {
+  __device__ __forceinline__ int t() const { return s_srv_req[0]; }
+  __device__ __forceinline__ int flags() const { return s_srv_req[1]; }
+  __device__ __forceinline__ uint32_t episode() const { return static_cast<uint32_t>(s_srv_req[2]); }
+};
+
+template <int MAXD>
+__global__ __launch_bounds__(64 * kNodesMaxWaves) void sc_nodes_server_kernel(const ScArgs a, int W, int E,
+                                                                               scg_sc_server_box* box,
+                                                                               uint32_t exit_seen, uint32_t idle_ticks) {
+  const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t* line = reinterpret_cast<const uint32_t*>(box);
+  uint32_t last = __hip_atomic_load(&box->done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t ex = exit_seen;
+  uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (w == 0) {
+      const uint32_t v = lane0 < 16 ? __hip_atomic_load(line + lane0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+      ex = __hip_atomic_load(&box->exit_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t q[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) q[i] = __builtin_amdgcn_readlane(v, i);
+      int cmd = 0;
+      if (ex != exit_seen) {
+        cmd = 2;
+      } else if (q[0] != last && q[7] == mailbox_check(q)) {
+        cmd = 1;
+        last = q[0];
+        if (lane0 == 0) {
+          s_srv_req[0] = static_cast<int32_t>(q[2]);
+          s_srv_req[1] = static_cast<int32_t>(q[3]);
+          s_srv_req[2] = static_cast<int32_t>(q[4]);
+        }
+      } else if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+        cmd = 2;
+      }
+      if (lane0 == 0) s_srv_req[3] = cmd;
+    }
+    __syncthreads();
+    const int cmd = __builtin_amdgcn_readfirstlane(s_srv_req[3]);
+    __syncthreads();  // every wave has read the command before wave 0 writes the next one
+    if (cmd == 2) break;
+    if (cmd == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    int lane;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
+    sc_nodes_tile<MAXD, true, false>(a, 0, lane, w, W, E, NodesServerStep{});
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every lane's stores before the answer
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&box->done_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    t0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (threadIdx.x == 0) __hip_atomic_store(&box->exit_seq, ex, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // LDS bytes of one block (the layout above); obs_bytes 4 (float) or 8 (double).
@@ -528,6 +614,38 @@ int sc_launch_nodes(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t 
     default: return fail(SCG_ERR_INVALID, "node-parallel kernel: nodes ship to at most 8 destinations");
   }
 #undef SCG_NODES_CASES
+}
+
+// The step server's block for a config the batch kernel runs (float64 observations, no
+// ledgers): one block of W waves with the batch kernel's LDS.
+int sc_launch_nodes_server(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t s, scg_sc_server_box* box,
+                           uint32_t exit_seen, uint32_t idle_ticks) {
+  if (W < 1 || W > kNodesMaxWaves) return fail(SCG_ERR_INVALID, "node-parallel server: %d waves per block", W);
+  if (!a.obs_f64 || a.led_v) return fail(SCG_ERR_INVALID, "the SupplyChain step server runs float64 observations, no ledgers");
+  const size_t lds = sc_nodes_lds_bytes(a.c.n_nodes, a.c.P, a.c.H, E, W, a.c.A, a.c.O, 8);
+  const size_t cap = sc_nodes_lds_max() - sizeof(s_srv_req);
+  if (lds > cap) return fail(SCG_ERR_INVALID, "node-parallel server: %zu B of LDS per block", lds);
+  static std::atomic<bool> raised[3][64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+#define SCG_SERVER_LAUNCH(D, K)                                                                                     \
+  if (lds > 64 * 1024 && !raised[K][dev].load(std::memory_order_acquire)) {                                         \
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sc_nodes_server_kernel<D>),                             \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(cap)) != hipSuccess)       \
+      return fail(SCG_ERR_HIP, "node-parallel server: cannot raise its LDS limit");                                 \
+    raised[K][dev].store(true, std::memory_order_release);                                                          \
+  }                                                                                                                 \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(sc_nodes_server_kernel<D>), dim3(1), dim3(64 * W), lds, s, a, W, E, box,       \
+                     exit_seen, idle_ticks);                                                                        \
+  break;
+  switch (maxd_bucket) {
+    case 2: SCG_SERVER_LAUNCH(2, 0)
+    case 4: SCG_SERVER_LAUNCH(4, 1)
+    case 8: SCG_SERVER_LAUNCH(8, 2)
+    default: return fail(SCG_ERR_INVALID, "node-parallel server: nodes ship to at most 8 destinations");
+  }
+#undef SCG_SERVER_LAUNCH
+  return check_launch("sc_nodes_server_kernel");
 }
 
 }  // namespace scg

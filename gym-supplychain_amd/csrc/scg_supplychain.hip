@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "scg_common.h"
+#include "scg_mailbox.h"
 
 // Diagnostic build only (-DSCG_SC_STAMPS, tools/sc_stamps.py): lane 0 of every wave of the
 // LDS lane kernel records the shader clock at phase boundaries into a buffer of its own
@@ -79,6 +80,8 @@ int sc_nodes_waves(int n_nodes);
 int sc_nodes_max_dests();
 size_t sc_nodes_lds_max();
 int sc_launch_nodes(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t s);
+int sc_launch_nodes_server(const ScArgs& a, int maxd_bucket, int W, int E, hipStream_t s, scg_sc_server_box* box,
+                           uint32_t exit_seen, uint32_t idle_ticks);
 
 __global__ __launch_bounds__(kScBlock) void sc_reset_kernel(const ScArgs a) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * kScBlock + threadIdx.x;
@@ -903,6 +906,122 @@ __attribute__((visibility("default"))) int scg_sc_debug_stamps(unsigned long lon
   return SCG_OK;
 }
 #endif
+
+// ---- step server (include/scgpu.h scg_sc_server_*) --------------------------------------
+static_assert(sizeof(scg_sc_server_box) == 128 && offsetof(scg_sc_server_box, done_seq) == 64, "SupplyChain mailbox");
+static_assert(sizeof(scg_sc_server) == 88, "SupplyChain server struct");
+static int sc_server_stop_now(scg_sc_server* sv) {
+  if (!sv->running) return SCG_OK;
+  __atomic_store_n(&sv->box_host->exit_req, sv->box_host->exit_req + 1, __ATOMIC_RELEASE);
+  sv->running = 0;
+  if (hipStreamSynchronize(static_cast<hipStream_t>(sv->stream)) != hipSuccess)
+    return fail(SCG_ERR_HIP, "SupplyChain step server: hipStreamSynchronize failed");
+  return SCG_OK;
+}
+
+int scg_sc_server_stop(scg_sc_server* sv) {
+  if (!sv || !sv->box_host || !sv->box_dev) return fail(SCG_ERR_INVALID, "null server/mailbox");
+  return sc_server_stop_now(sv);
+}
+
+static int sc_server_launch(const scg_sc_config* cfg, const scg_sc_state* st, scg_sc_server* sv) {
+  ScArgs a = sc_args(cfg, st);
+  a.act = sv->action;
+  a.obs = sv->obs;
+  a.rew = sv->reward;
+  a.term_obs = nullptr;
+  const uint32_t exit_seen = __atomic_load_n(&sv->box_host->exit_req, __ATOMIC_ACQUIRE);
+  if (int rc = sc_launch_nodes_server(a, sc_maxd_bucket(cfg->max_dests), cfg->group, cfg->inbox_size,
+                                      static_cast<hipStream_t>(sv->stream), sv->box_dev, exit_seen,
+                                      static_cast<uint32_t>(sv->idle_us) * 100u))
+    return rc;
+  sv->running = 1;
+  sv->launches += 1;
+  sv->last_ns = mono_ns();
+  return SCG_OK;
+}
+
+int scg_sc_server_post(const scg_sc_config* cfg, scg_sc_state* st, scg_sc_server* sv) {
+  if (int rc = sc_check(cfg, st)) return rc;
+  if (!sv || !sv->box_host || !sv->box_dev || !sv->action || !sv->obs || !sv->reward)
+    return fail(SCG_ERR_INVALID, "SupplyChain step server: mailbox, action, obs and reward are required");
+  if (!sv->stream) return fail(SCG_ERR_INVALID, "SupplyChain step server: needs a (non-blocking) stream of its own");
+  if (sv->idle_us < 100 || sv->idle_us > 10000000) return fail(SCG_ERR_INVALID, "idle_us outside 100..10^7");
+  if (st->n_envs > kScBlock) return fail(SCG_ERR_INVALID, "the SupplyChain step server runs up to %d envs", kScBlock);
+  if (cfg->kernel != SCG_SC_KERNEL_NODES || cfg->layout != SCG_SC_LAYOUT_ENV_FASTEST || cfg->inbox_size < 0)
+    return fail(SCG_ERR_INVALID, "the SupplyChain step server runs the node-parallel kernel's configs");
+  if (!cfg->obs_f64 || st->ledger) return fail(SCG_ERR_INVALID, "the SupplyChain step server runs float64 observations, no ledgers");
+  if (st->time_step < 0) return fail(SCG_ERR_NOT_RESET, "step() before reset()");
+  const int T = cfg->total_time_steps;
+  if (st->time_step >= T) return fail(SCG_ERR_PAST_HORIZON, "step() after the terminal step %d", T);
+  scg_sc_server_box* b = sv->box_host;
+  if (__atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != sv->seq)
+    return fail(SCG_ERR_INVALID, "SupplyChain step server: a post while the last request is unanswered");
+  const int t = st->time_step + 1;
+  // a block idle for more than half its time-out may be exiting: retire it before posting
+  if (sv->running && mono_ns() - sv->last_ns > static_cast<int64_t>(sv->idle_us) * 500)
+    if (int rc = sc_server_stop_now(sv)) return rc;
+  uint32_t line[16] = {0};
+  const uint32_t seq = sv->seq + 1;
+  line[0] = seq;
+  line[2] = static_cast<uint32_t>(t);
+  line[3] = t == T ? 1u : 0u;
+  line[4] = st->episode;
+  line[7] = mailbox_check(line);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(b);
+  for (int i = 1; i < 16; ++i) __atomic_store_n(&dst[i], line[i], __ATOMIC_RELAXED);
+  __atomic_store_n(&dst[0], seq, __ATOMIC_RELEASE);
+  sv->seq = seq;
+  sv->t = t;
+  sv->done = t == T ? 1 : 0;
+  sv->last_ns = mono_ns();
+  if (!sv->running)
+    if (int rc = sc_server_launch(cfg, st, sv)) return rc;
+  return SCG_OK;
+}
+
+int scg_sc_server_wait(const scg_sc_config* cfg, scg_sc_state* st, scg_sc_server* sv, int64_t spin_us, int32_t* done) {
+  if (int rc = sc_check(cfg, st)) return rc;
+  if (!sv || !sv->box_host) return fail(SCG_ERR_INVALID, "null server/mailbox");
+  scg_sc_server_box* b = sv->box_host;
+  const uint32_t seq = sv->seq;
+  const int64_t start = mono_ns();
+  const int64_t check_ns = (sv->check_us > 0 ? sv->check_us : 2000000) * int64_t(1000);
+  int64_t check = start + check_ns;
+  int gone = 0;
+  for (uint32_t spins = 0;; ++spins) {
+    if (__atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) == seq) break;
+    cpu_relax();
+    if ((spins & 255u) != 255u) continue;
+    const int64_t now = mono_ns();
+    if (spin_us >= 0 && now - start > spin_us * 1000) return SCG_PENDING;
+    if (now < check) continue;
+    check = now + check_ns;
+    // the BeerGame server's checks (scg_bg_server_wait): a HIP error at once; a block gone
+    // without answering launched again once (it serves the pending request first)
+    const hipError_t q = hipStreamQuery(static_cast<hipStream_t>(sv->stream));
+    if (q != hipSuccess && q != hipErrorNotReady)
+      return fail(SCG_ERR_HIP, "SupplyChain step server: the stream reports %s (step %d)", hipGetErrorString(q), sv->t);
+    if (__atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) == seq) break;
+    if (q == hipSuccess) {
+      if (gone++ > 0)
+        return fail(SCG_ERR_HIP, "SupplyChain step server: the block exits without answering (step %d)", sv->t);
+      sv->running = 0;
+      sv->relaunches += 1;
+      if (int rc = sc_server_launch(cfg, st, sv)) return rc;
+    }
+    if (now - start > 60000000000LL) return fail(SCG_ERR_HIP, "SupplyChain step server: no answer for 60 s (step %d)", sv->t);
+  }
+  sv->last_ns = mono_ns();
+  st->time_step = sv->t;  // no auto-reset on this path
+  if (done) *done = sv->done;
+  return SCG_OK;
+}
+
+int scg_sc_server_step(const scg_sc_config* cfg, scg_sc_state* st, scg_sc_server* sv, int32_t* done) {
+  if (int rc = scg_sc_server_post(cfg, st, sv)) return rc;
+  return scg_sc_server_wait(cfg, st, sv, -1, done);
+}
 
 int scg_sc_draw_tables(const scg_sc_config* cfg, const scg_sc_state* st, uint32_t episode, int32_t* demand,
                        int32_t* leadtimes, void* stream) {

@@ -138,6 +138,23 @@ class BgServerSlot(ctypes.Structure):
                 ("done", ctypes.c_int32), ("relaunches", ctypes.c_int32)]
 
 
+class ScServerBox(ctypes.Structure):
+    """scg_sc_server_box (include/scgpu.h): the SupplyChain step server's mailbox."""
+    _fields_ = [("req_seq", ctypes.c_uint32), ("cmd", ctypes.c_int32), ("t", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("episode", ctypes.c_uint32), ("pad0", ctypes.c_int32 * 2), ("check", ctypes.c_uint32),
+                ("pad1", ctypes.c_int32 * 8), ("done_seq", ctypes.c_uint32), ("exit_req", ctypes.c_uint32),
+                ("exit_seq", ctypes.c_uint32), ("pad2", ctypes.c_uint32 * 13)]
+
+
+class ScServer(ctypes.Structure):
+    """scg_sc_server (include/scgpu.h): the SupplyChain step server of one drop-in env."""
+    _fields_ = [("box_host", ctypes.c_void_p), ("box_dev", ctypes.c_void_p), ("stream", ctypes.c_void_p),
+                ("action", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p),
+                ("idle_us", ctypes.c_int32), ("check_us", ctypes.c_int32), ("running", ctypes.c_int32),
+                ("seq", ctypes.c_uint32), ("t", ctypes.c_int32), ("done", ctypes.c_int32), ("last_ns", ctypes.c_int64),
+                ("launches", ctypes.c_int64), ("relaunches", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
 # scg_bg_slab_field: word offsets of a BeerGame state slab (scg_bg_slab_layout)
 (SLAB_ERROR, SLAB_INVENTORY, SLAB_BACKLOG, SLAB_ORDERS, SLAB_INV_COSTS, SLAB_BACKLOG_COSTS, SLAB_TERMINAL_OBS,
  SLAB_RING, SLAB_EPISODE_RETURN, SLAB_FINAL_RETURN, SLAB_HISTORY, SLAB_TOTAL, SLAB_FIELDS) = range(13)
@@ -244,6 +261,12 @@ SIGNATURES = {
     "scg_sc_draw_tables": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.c_uint32,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "scg_sc_nodes_max_blocks": (ctypes.c_int, [ctypes.c_int32]),
+    "scg_sc_server_post": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.POINTER(ScServer)]),
+    "scg_sc_server_wait": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.POINTER(ScServer),
+                                          ctypes.c_int64, _i32p]),
+    "scg_sc_server_step": (ctypes.c_int, [ctypes.POINTER(ScConfig), ctypes.POINTER(ScState), ctypes.POINTER(ScServer),
+                                          _i32p]),
+    "scg_sc_server_stop": (ctypes.c_int, [ctypes.POINTER(ScServer)]),
     "scg_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_void_p]),
     "scg_uniform_ints": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,

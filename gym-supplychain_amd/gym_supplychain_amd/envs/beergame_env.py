@@ -24,6 +24,7 @@ import torch
 from .. import _native as nat
 from .. import checkpoint as ckpt
 from .. import spaces
+from . import resident
 from ..distributed import entropy_seed
 
 # beergame_env.py:16-23
@@ -547,7 +548,8 @@ class _StepServer:
     process, whatever the number of drop-in envs (up to BG_SERVER_SLOTS per server; more
     start another server): many envs stepped in turn share one resident wave and one stream.
     The high priority puts the stream on a hardware queue of its own pool, so the parked wave
-    never holds up work of normal-priority streams that would share its queue. The wave exits
+    never holds up work of normal-priority streams that would share its queue; and at most one
+    server per device is resident at a time (envs/resident.py). The wave exits
     when stopped, or by itself after IDLE_US without a request; a post launches it again when
     needed. The mailbox is freed only after the wave has been stopped."""
 
@@ -567,23 +569,11 @@ class _StepServer:
         raise RuntimeError("too many drop-in envs on one device for the step server")
 
     def __init__(self, device, levels, demand_mode, key):
-        hip = nat.hip_runtime()
-        hip.hipStreamCreateWithPriority.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint, ctypes.c_int]
-        hip.hipDeviceGetStreamPriorityRange.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
-        hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
-        stream = ctypes.c_void_p()
-        with torch.cuda.device(device):
-            least, greatest = ctypes.c_int(0), ctypes.c_int(0)
-            if hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest)) != 0:
-                greatest.value = 0
-            # hipStreamNonBlocking, the highest priority the device offers
-            if hip.hipStreamCreateWithPriority(ctypes.byref(stream), 1, greatest.value) != 0:
-                raise RuntimeError("hipStreamCreateWithPriority failed")
-        self._hip, self._device, self._key = hip, device, key
-        self.priority = greatest.value
+        stream, self.priority = resident.server_stream(device)
+        self._device, self._dev_index, self._key = device, key[0], key
         self._box = box = nat.MappedBuffer(ctypes.sizeof(nat.BgServerBox))
         self.box = nat.BgServerBox.from_address(box.host)
-        self.sv = nat.BgServer(box.host, box.dev, stream.value, levels, demand_mode, self.IDLE_US, 0)
+        self.sv = nat.BgServer(box.host, box.dev, stream, levels, demand_mode, self.IDLE_US, 0)
         self._closed = False
 
     @property
@@ -600,7 +590,8 @@ class _StepServer:
             return
         self.stop()  # raises if the wave cannot be stopped: then the mailbox stays allocated
         self._closed = True
-        self._hip.hipStreamDestroy(ctypes.c_void_p(self.sv.stream))
+        resident.release(self._dev_index, self)
+        resident.destroy_stream(self.sv.stream)
         self._box = None
         if _SERVERS.get(self._key) is self:
             del _SERVERS[self._key]
@@ -616,12 +607,14 @@ class _ServerSlot:
         nat.check(nat.lib.scg_bg_server_attach(ctypes.byref(server.sv), ctypes.byref(self.slot)))
         self._args = (vec._cfg_addr, vec._st_addr, ctypes.addressof(self.slot))
         self._fast = nat.fast.bg_server_step
+        self._claim = (server._dev_index, server)
 
     @property
     def sv(self):
         return self.server.sv
 
     def step(self):
+        resident.claim(*self._claim)
         return self._fast(*self._args)
 
     def close(self):

@@ -19,8 +19,11 @@ Differences from the reference:
   * build_info=True keeps info['sc_episode'] on the device (lane and staged kernels); the
     drop-in env returns it with the reference's per-entry NumPy types.
 """
+import atexit
 import ctypes
 import hashlib
+import os
+import weakref
 
 import numpy as np
 import torch
@@ -29,6 +32,7 @@ from .. import _native as nat
 from .. import checkpoint as ckpt
 from .. import spaces
 from . import demand
+from . import resident
 from ..distributed import entropy_seed
 
 _MAXP = nat.SC_MAX_PRODUCTS
@@ -638,6 +642,68 @@ class SC_NodeView:
         return f"{self.label} ({self.shipments_by_prod}) [{np.round(self.stock, 1)}]"
 
 
+class _ScStepServer:
+    """The drop-in SupplyChainEnv's step server (include/scgpu.h scg_sc_server_*): one
+    resident block of the node-parallel kernel's shape on a non-blocking, high-priority stream
+    of its own polls a host-mapped mailbox and runs each posted step on the env's state (the
+    batch kernel's tile code), writing observation and reward to the env's host-mapped block.
+    It exits when stopped (reset(), close(), another server of the device becoming resident,
+    interpreter exit) or by itself after IDLE_US without a request; step() launches it again
+    when needed. The mailbox is freed only after the block has been stopped."""
+
+    IDLE_US = 20000
+
+    def __init__(self, vec, act_dev, obs_dev, rew_dev):
+        stream, self.priority = resident.server_stream(vec.device)
+        self._dev_index = vec._dev_index
+        self._device = vec.device
+        self._box = box = nat.MappedBuffer(ctypes.sizeof(nat.ScServerBox))
+        self.box = nat.ScServerBox.from_address(box.host)
+        self.sv = nat.ScServer(box.host, box.dev, stream, act_dev, obs_dev, rew_dev, self.IDLE_US, 0)
+        self._args = (vec._cfg_addr, vec._st_addr, ctypes.addressof(self.sv))
+        self._fast = nat.fast.sc_server_step
+        self._closed = False
+        _SC_SERVERS.add(self)
+
+    @property
+    def launches(self):
+        return int(self.sv.launches)
+
+    def step(self):
+        resident.claim(self._dev_index, self)
+        return self._fast(*self._args)
+
+    def stop(self):
+        if not self._closed:
+            with torch.cuda.device(self._device):
+                nat.check(nat.lib.scg_sc_server_stop(ctypes.byref(self.sv)))
+
+    def close(self):
+        if self._closed:
+            return
+        self.stop()  # raises if the block cannot be stopped: then the mailbox stays allocated
+        self._closed = True
+        resident.release(self._dev_index, self)
+        resident.destroy_stream(self.sv.stream)
+        self._box = None
+        _SC_SERVERS.discard(self)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass
+
+
+_SC_SERVERS = weakref.WeakSet()
+
+
+@atexit.register
+def _stop_sc_servers():  # no server block outlives the interpreter (nor its mailbox)
+    for sv in list(_SC_SERVERS):
+        sv.close()
+
+
 class SupplyChainEnv(spaces.Env):
     """Drop-in for gym_supplychain.envs.SupplyChainEnv (:478-813), one env on the GPU.
 
@@ -654,7 +720,11 @@ class SupplyChainEnv(spaces.Env):
     `count_leadtimes_per_timestep` and `rand_generator` are kept.
     kernel=None (default): the node-parallel kernel when the chain qualifies (one env is a
     latency path: every node on its own wave), else the vec env's "auto" choice; or name one
-    ("lane", "staged", "level", "nodes", "auto").
+    ("lane", "staged", "level", "nodes", "auto"). On the node-parallel kernel without
+    build_info each step is posted to a resident block (the step server, include/scgpu.h
+    scg_sc_server_*) rather than launched; the block exits 20 ms after the last step, so a
+    device-wide torch.cuda.synchronize() right after a step waits up to that long.
+    SCG_SC_SERVER=0 launches the kernel per step instead.
     """
 
     def __init__(self, nodes_info, num_products=1, unmet_demand_cost=1000, exceeded_stock_capacity_cost=1000,
@@ -728,6 +798,12 @@ class SupplyChainEnv(spaces.Env):
         self._sync = nat.stream_synchronize_fn()
         self.build_info = spec.build_info
         self.est_episode = None
+        # On the node-parallel kernel (float64 observations, no ledgers) the step runs on a
+        # resident block polling a mailbox (scg_sc_server_*): no launch and no stream
+        # synchronisation per step. SCG_SC_SERVER=0: one launch plus one synchronisation.
+        self._server = None
+        if os.environ.get("SCG_SC_SERVER", "1") != "0" and self._vec.kernel == "nodes" and not self.build_info:
+            self._server = _ScStepServer(self._vec, *self._io_ptrs)
 
     @property
     def time_step(self):
@@ -781,14 +857,19 @@ class SupplyChainEnv(spaces.Env):
             raise IndexError(f"action has {a.size} values, the chain needs {n}")
         self._act_np[0, :] = a[:n]  # like the reference, values beyond the chain's actions are unused
         v = self._vec
-        stream = nat.raw_stream(v._dev_index)
-        act, obs, rew = self._io_ptrs
-        r = nat.fast.sc_step(v._cfg_addr, v._st_addr, act, obs, rew, v._term_ptr, v._flags, stream)
-        if r > 1:
-            nat.check(r >> 1)
-        rc = self._sync(stream)
-        if rc:
-            raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
+        if self._server is not None:
+            r = self._server.step()  # returns once the block has written obs and reward
+            if r > 1:
+                nat.check(r >> 1)
+        else:
+            stream = nat.raw_stream(v._dev_index)
+            act, obs, rew = self._io_ptrs
+            r = nat.fast.sc_step(v._cfg_addr, v._st_addr, act, obs, rew, v._term_ptr, v._flags, stream)
+            if r > 1:
+                nat.check(r >> 1)
+            rc = self._sync(stream)
+            if rc:
+                raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
         self.current_state = self._obs_np.copy()
         self.current_reward = np.float64(self._rew_np[0])
         self.episode_rewards += self.current_reward
@@ -816,4 +897,12 @@ class SupplyChainEnv(spaces.Env):
         print('Current reward:', round(float(self.current_reward), 3))
 
     def close(self):
-        pass
+        server = getattr(self, "_server", None)
+        if server is not None:
+            server.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass

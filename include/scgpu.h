@@ -40,7 +40,8 @@ extern "C" {
  * 6 (round 5): the BeerGame step server (scg_bg_server_box, scg_bg_server, scg_bg_server_step,
  *   scg_bg_server_stop) and the testing hook scg_sc_nodes_max_blocks.
  * 7 (round 6): the step server serves up to SCG_BG_SERVER_SLOTS envs from one wave
- *   (scg_bg_server_slot, attach / detach / post / wait), mixing-hash check word. */
+ *   (scg_bg_server_slot, attach / detach / post / wait), mixing-hash check word; the
+ *   SupplyChain step server (scg_sc_server_box, scg_sc_server, scg_sc_server_*). */
 #define SCG_ABI_VERSION 7
 
 #if defined(__GNUC__)
@@ -537,6 +538,63 @@ SCG_API int scg_sc_step(const scg_sc_config* cfg, scg_sc_state* st, const float*
  * [N][T+1][R][P], leadtimes DEVICE int32 [N][T][n_leadtimes] (NULL when deterministic). */
 SCG_API int scg_sc_draw_tables(const scg_sc_config* cfg, const scg_sc_state* st, uint32_t episode,
                                int32_t* demand, int32_t* leadtimes, void* stream);
+
+/*
+ * Step server for the drop-in SupplyChainEnv (one env stepped per Python call,
+ * supplychain_env.py:703-748): one resident block of the node-parallel kernel's shape (a wave
+ * per node) polls a host-mapped mailbox and runs the node-parallel step of tile 0 for each
+ * posted step, on the state and buffers the launch arguments named when it started — the
+ * config's kernel must be SCG_SC_KERNEL_NODES, float64 observations, no ledgers, up to 64
+ * envs. The same protocol as the BeerGame server: post the step (its time, flags and
+ * episode travel in the request line), wait for the answer word; the block exits on
+ * scg_sc_server_stop or after idle_us without a request, and the next post launches it
+ * again (with the then-current state pointers and action / obs / reward buffers).
+ */
+typedef struct scg_sc_server_box { /* host-mapped (hipHostMalloc mapped + coherent), 128 B */
+  uint32_t req_seq;   /* request number                                                   */
+  int32_t cmd;        /* 0: step                                                          */
+  int32_t t;          /* the step's time (1..T)                                           */
+  int32_t flags;      /* bit0 terminal (as scg_sc_step's kernel flags)                    */
+  uint32_t episode;   /* the state's episode                                              */
+  int32_t pad0[2];
+  uint32_t check;     /* scg mixing hash of the line's other 15 words                     */
+  int32_t pad1[8];
+  uint32_t done_seq;  /* the last request served (written by the block)                   */
+  uint32_t exit_req;  /* the block exits when this differs from its launch value          */
+  uint32_t exit_seq;  /* written by the block as it exits: the exit_req it saw last       */
+  uint32_t pad2[13];
+} scg_sc_server_box;
+
+typedef struct scg_sc_server {
+  scg_sc_server_box* box_host; /* the mailbox's host address                              */
+  scg_sc_server_box* box_dev;  /* its device address                                      */
+  void* stream;                /* a non-blocking stream of the caller's (high priority)   */
+  const float* action;         /* DEVICE-visible float32 [N][A]                           */
+  void* obs;                   /* DEVICE-visible float64 [N][O]                           */
+  double* reward;              /* DEVICE-visible float64 [N]                              */
+  int32_t idle_us;             /* the block exits after this long without a request       */
+  int32_t check_us;            /* a waiting step checks this often for a gone block (0: 2 s) */
+  /* host bookkeeping: zero before first use */
+  int32_t running;
+  uint32_t seq;                /* the request last posted                                 */
+  int32_t t;                   /* the step it runs                                        */
+  int32_t done;                /* that step is the terminal one                           */
+  int64_t last_ns;
+  int64_t launches;
+  int32_t relaunches;
+  int32_t pad;
+} scg_sc_server;
+
+/* Post step(action) of the st->n_envs <= 64 envs (launches the block if needed). */
+SCG_API int scg_sc_server_post(const scg_sc_config* cfg, scg_sc_state* st, scg_sc_server* sv);
+/* Wait for it: SCG_OK (st->time_step advanced, *done), SCG_PENDING after spin_us (< 0: no
+ * limit; the wait then fails after 60 s), or an error. */
+SCG_API int scg_sc_server_wait(const scg_sc_config* cfg, scg_sc_state* st, scg_sc_server* sv, int64_t spin_us,
+                               int32_t* done);
+/* post + wait without limit. */
+SCG_API int scg_sc_server_step(const scg_sc_config* cfg, scg_sc_state* st, scg_sc_server* sv, int32_t* done);
+/* Ask the block to exit and wait for it (a no-op when it is not running). */
+SCG_API int scg_sc_server_stop(scg_sc_server* sv);
 
 /* Testing hook: cap the node-parallel kernel's persistent grid at `blocks` blocks (0, the
  * default: as many as the device holds at once), so a small batch runs several 64-env tiles

@@ -14,7 +14,9 @@ of the reference step() on one host core.
   DummyVecEnv of drop-in envs): every env holds a slot of the one shared server, so the 8
   share one resident wave; per step() call, on the server and on the launch path.
 * SupplyChain2perStageEnv.step (supplychain_env.py:703-748; reference ~136 us per step):
-  the same host-mapped path, host RandomState episode draws (the reference's), float64 obs.
+  its step server (a resident block of the node-parallel kernel polling a host-mapped
+  mailbox, scg_sc_server_*) and the launch path (SCG_SC_SERVER=0), host RandomState episode
+  draws (the reference's), float64 obs.
 * cpu: oracle.beergame.BeerGameOracle.step and oracle.supplychain.SupplyChainOracle.step
   (the calibrated NumPy ports of the reference step, profiles/r04_cpu_calibration.json) on
   this box's host, one core.
@@ -138,14 +140,19 @@ def beergame_copies(episodes):
     return _stats(_time_episodes(env, acts, episodes, 35))
 
 
-def supplychain(episodes):
+def supplychain(episodes, server=True):
     import numpy as np
+    os.environ["SCG_SC_SERVER"] = "1" if server else "0"
     import gym_supplychain_amd as gsa
     env = gsa.make("sc-2perstage-v0", seed=0)
     rng = np.random.RandomState(0)
     acts = [rng.uniform(-1, 1, env.action_space.shape).astype(np.float32) for _ in range(720)]
     _time_episodes(env, acts, 1, 360)
-    return _stats(_time_episodes(env, acts, episodes, 360)), env._vec.kernel
+    st = _stats(_time_episodes(env, acts, episodes, 360))
+    if server:
+        st["server_block_launches"] = env._server.launches
+    env.close()
+    return st, env._vec.kernel
 
 
 def cpu_beergame(episodes):
@@ -207,7 +214,11 @@ def main():
          beergame_many(max(a.bg_episodes // 8, 4), server=False))
     emit("BeerGameEnv.step, round-4 design (H2D copy, launch, 2 D2H copies, sync)", 12.8, beergame_copies(a.bg_episodes))
     st, kernel = supplychain(a.sc_episodes)
-    emit("SupplyChain2perStageEnv.step (host-mapped io, one launch + stream sync)", 136.0, st, kernel=kernel)
+    emit("SupplyChain2perStageEnv.step (step server: resident block, host-mapped mailbox and io)", 136.0, st,
+         kernel=kernel)
+    st, kernel = supplychain(a.sc_episodes, server=False)
+    emit("SupplyChain2perStageEnv.step, launch path (SCG_SC_SERVER=0: host-mapped io, one launch + stream sync)",
+         136.0, st, kernel=kernel)
     if not a.no_cpu:
         emit("cpu: oracle.beergame.BeerGameOracle.step, one host core", 12.8, cpu_beergame(a.bg_episodes))
         emit("cpu: oracle.supplychain.SupplyChainOracle.step, one host core", 136.0, cpu_supplychain(a.sc_episodes))

@@ -54,6 +54,8 @@ def main():
         torch.cuda.synchronize()
         assert fn(buf.ctypes.data, buf.shape[0]) == 0
         st = buf.astype(np.int64)
+        # a persistent grid writes one record per (resident block, wave): the rest stay zero
+        st = st[st[:, 4] != 0]
         t0 = st[:, 0].min()
         rel = st[:, :8] - t0
         out = {"step": s, "build_info": a.build_info, "waves": int(len(st)), "span": int(rel[:, 4].max()),
@@ -65,7 +67,20 @@ def main():
         out["phase_p50_p90"] = {n: [int(np.percentile(d[:, k], 50)), int(np.percentile(d[:, k], 90))]
                                 for k, n in enumerate(names)}
         wi = np.arange(len(st)) % W
-        out["by_wave_p50"] = {n: [int(np.median(d[wi == w, k])) for w in range(W)] for k, n in enumerate(names)}
+        out["by_wave_p50"] = bw = {n: [int(np.median(d[wi == w, k])) for w in range(W)] for k, n in enumerate(names)}
+        # The step's dependency graph against its barrier schedule (per-wave p50, wave w = node
+        # w): the barriers make a tile cost the sum over phases of the slowest wave; without
+        # them, a node's heaps would wait only for its own act and its sources' acts (the
+        # inbox), and a node's act for the action tile and every wave's flags (barrier 0 stays).
+        if W == 8 and a.envs >= 64:
+            src = {2: (0, 1), 3: (0, 1), 4: (2, 3), 5: (2, 3), 6: (4, 5), 7: (4, 5)}  # sc-2perstage
+            S, A, Hh, O = bw["stage"], bw["act"], bw["heaps"], bw["out"]
+            sched = max(S) + max(A) + max(Hh) + max(O)
+            act_end = [max(S) + A[i] for i in range(W)]
+            heaps_end = [max([act_end[i]] + [act_end[j] for j in src.get(i, ())]) + Hh[i] for i in range(W)]
+            out["critical_path_clocks"] = {"barrier_schedule": int(sched),
+                                           "dependency_graph_keeping_barrier0": int(max(heaps_end) + max(O)),
+                                           "mean_wave_work": int(np.mean(S) + np.mean(A) + np.mean(Hh) + np.mean(O))}
         # real-time clock (100 MHz, one clock for the whole chip): the launch's timeline in us
         rt = (st[:, 8:10] - st[:, 8].min()) / 100.0
         blk = np.arange(len(st)) // W
