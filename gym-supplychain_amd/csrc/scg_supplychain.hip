@@ -909,7 +909,7 @@ __attribute__((visibility("default"))) int scg_sc_debug_stamps(unsigned long lon
 
 // ---- step server (include/scgpu.h scg_sc_server_*) --------------------------------------
 static_assert(sizeof(scg_sc_server_box) == 128 && offsetof(scg_sc_server_box, done_seq) == 64, "SupplyChain mailbox");
-static_assert(sizeof(scg_sc_server) == 88, "SupplyChain server struct");
+static_assert(sizeof(scg_sc_server) == 96, "SupplyChain server struct");
 static int sc_server_stop_now(scg_sc_server* sv) {
   if (!sv->running) return SCG_OK;
   __atomic_store_n(&sv->box_host->exit_req, sv->box_host->exit_req + 1, __ATOMIC_RELEASE);

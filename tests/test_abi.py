@@ -353,3 +353,16 @@ def test_prepare_full_table_limits():
     assert rc == nat.SCG_ERR_INVALID and "shipment_delays" in nat.last_error()
     rc, _, _ = _prepare_full([2] * 36, 35, variant=2)
     assert rc == nat.SCG_ERR_INVALID and "full_table" in nat.last_error()
+
+
+def test_server_struct_layouts_match_the_library():
+    """The step servers' structs as ctypes lays them out are the sizes the library asserts at
+    compile time (scg_beergame.hip, scg_supplychain.hip static_asserts), so a binding that
+    drifted from include/scgpu.h fails here rather than on the GPU."""
+    from gym_supplychain_amd import _native as nat
+    assert ctypes.sizeof(nat.BgServerLine) == 64
+    assert ctypes.sizeof(nat.BgServerBox) == 17 * 64 + 64 + nat.BG_SERVER_SLOTS * nat.BG_SERVER_ARGS_BYTES
+    assert nat.BgServerBox.done_seq.offset == 16 * 64 and nat.BgServerBox.args.offset == 18 * 64
+    assert ctypes.sizeof(nat.BgServer) == 72 and ctypes.sizeof(nat.BgServerSlot) == 64
+    assert ctypes.sizeof(nat.ScServerBox) == 128 and nat.ScServerBox.done_seq.offset == 64
+    assert ctypes.sizeof(nat.ScServer) == 96
