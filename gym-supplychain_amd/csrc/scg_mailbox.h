@@ -1,7 +1,7 @@
 // The step servers' mailbox protocol (include/scgpu.h scg_bg_server_*, scg_sc_server_*),
-// shared by the BeerGame and SupplyChain servers: a request is one 64-byte line of
-// host-mapped memory, 16 words, word 7 a mixing hash of the other 15 (multiply, xor and
-// rotate per word), so a read of the line that mixes two requests is detected whatever the
+// shared by the BeerGame and SupplyChain servers: a request is one (or two) 64-byte lines of
+// host-mapped memory, 16 (32) words, word 7 a mixing hash of the others (multiply, xor and
+// rotate per word), so a read of the lines that mixes two requests is detected whatever the
 // words' differences; and the host's clock and spin hint.
 #pragma once
 
@@ -10,9 +10,10 @@
 
 namespace scg {
 
-__host__ __device__ inline uint32_t mailbox_check(const uint32_t (&w)[16]) {
+template <int N>
+__host__ __device__ inline uint32_t mailbox_check(const uint32_t (&w)[N]) {
   uint32_t h = 0x9E3779B9u;
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < N; ++i) {
     if (i == 7) continue;
     h ^= w[i] * 0x85EBCA6Bu + static_cast<uint32_t>(i);
     h = (h << 13) | (h >> 19);

@@ -153,12 +153,18 @@ struct TileWalk {
 // One tile of 64 envs (tile * 64 ...): the step described at the top, on the kernel arguments
 // `a`, except the step's time, flags and episode, which come from `sp` (sp.t(), sp.flags(),
 // sp.episode(): the batch kernel's launch arguments, read where used as before; the step
-// server's request). lane is the thread's lane, opaque to the compiler; w the wave index.
+// server's request), and the action rows (sp.act(a)). With sp.keep_state() the stage reads no
+// state: the step server's block stepped this env last and its LDS still holds the stocks,
+// sizes, heaps and episode return that step left. lane is the thread's lane, opaque to the
+// compiler; w the wave index.
 struct NodesLaunchStep {  // the batch kernel: the step fields of the launch arguments
+  static constexpr bool kKeepsState = false;
   const ScArgs& a;
   __device__ __forceinline__ int t() const { return a.t; }
   __device__ __forceinline__ int flags() const { return a.flags; }
   __device__ __forceinline__ uint32_t episode() const { return a.episode; }
+  __device__ __forceinline__ const float* act(const ScArgs& x) const { return x.act; }
+  __device__ __forceinline__ bool keep_state() const { return false; }
 };
 
 template <int MAXD, bool F64, bool LED, class Step>
@@ -225,17 +231,23 @@ __device__ __forceinline__ void sc_nodes_tile(const ScArgs& a, int64_t tile, int
   bool bad = false;
   {
     constexpr int kAct = 4;  // action elements per thread per round
-    const float* src = a.act + n0 * c.A;
+    const float* src = sp.act(a) + n0 * c.A;
     const int na = nb * c.A;
+    // the step server's state kept in LDS since its previous request (NodesServerStep)
+    const bool keep = sp.keep_state();
     float av[kAct];
 #pragma unroll
     for (int u = 0; u < kAct; ++u)
       if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) av[u] = src[threadIdx.x + u * blockDim.x];
-    const double r0 = (w == 0 && live && a.ep_ret) ? a.ep_ret[n] : 0.0;
+    const double r0 = (w == 0 && live && a.ep_ret && !keep) ? a.ep_ret[n] : 0.0;
     for (int i = w; i < NN; i += W)
       for (int p = 0; p < P; ++p) {
         const int hp = i * P + p;
         if (!live) continue;
+        if (keep) {  // stocks, sizes and heaps are this env's, as the last step left them
+          bad |= !sc_recv_scan(lheap(hp), hsz[hp * 64 + lane], sp.t(), recv[hp * 64 + lane]);
+          continue;
+        }
         const int64_t r = static_cast<int64_t>(hp) * a.n + n;
         const double st = a.stock[r];
         const int32_t sz = a.size[r];
@@ -256,7 +268,7 @@ __device__ __forceinline__ void sc_nodes_tile(const ScArgs& a, int64_t tile, int
         if (static_cast<int>(threadIdx.x) + u * static_cast<int>(blockDim.x) < na) act_t[tw.r * Ap + tw.k] = av[u];
       for (int q = threadIdx.x + kAct * blockDim.x; q < na; q += blockDim.x, tw.next()) act_t[tw.r * Ap + tw.k] = src[q];
     }
-    if (w == 0 && live && a.ep_ret) ret0[lane] = r0;
+    if (w == 0 && live && a.ep_ret && !keep) ret0[lane] = r0;
   }
   amb[w * 64 + lane] = bad ? 1 : 0;
   NSTAMP(5);
@@ -347,6 +359,7 @@ __device__ __forceinline__ void sc_nodes_tile(const ScArgs& a, int64_t tile, int
       const double r = ret0[lane] + reward;  // episode_rewards += current_reward (:739)
       if (terminal && a.final_ret) a.final_ret[n] = r;
       a.ep_ret[n] = autoreset ? 0.0 : r;
+      if constexpr (Step::kKeepsState) ret0[lane] = autoreset ? 0.0 : r;  // the next request's
     }
     for (int k = 0; k < c.R * c.P; ++k) sc_observe_demand(c, g, sp.t(), k, sink);  // (:771)
     sc_observe_tail(c, sp.t(), sink);                                               // (:786)
@@ -432,19 +445,26 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
 }
 
 // ---- step server for the drop-in SupplyChainEnv (include/scgpu.h scg_sc_server_*) --------
-// One block of the batch kernel's shape, resident: wave 0 polls the mailbox's request line
-// (lanes 0-15, system scope, with the exit word) and puts what it found in LDS; after a
-// barrier every wave either exits, sleeps and polls again, or runs tile 0 of the step with
-// the request's time, flags and episode (NodesServerStep) — the batch kernel's code — and
-// then lane 0 publishes the request number with a system-scope release store. At launch the
+// One block of the batch kernel's shape, resident: wave 0 polls the mailbox's request lines
+// (the request and the inline action row, lanes 0-31, system scope, with the exit word) and
+// puts what it found in LDS; after a barrier every wave either exits, sleeps and polls again,
+// or runs tile 0 of the step with the request's time, flags, episode and action row
+// (NodesServerStep) — the batch kernel's code, minus the state loads when the block's LDS
+// still holds the state of this env's previous step — and then lane 0 publishes the request
+// number with a system-scope release store. At launch the
 // last request served is the answer word, so a request posted while no block ran is served
 // first. It exits when exit_req changes or after idle_ticks of the 100 MHz real-time clock
 // without a request, and writes the exit word it saw as it goes.
-__shared__ int32_t s_srv_req[4];  // t, flags, episode, command (0 none, 1 step, 2 exit)
+__shared__ int32_t s_srv_req[5];  // t, flags, episode, command (0 none, 1 / 3 step, 2 exit), keep
+__shared__ float s_srv_act[16];   // env 0's action row when it travelled in the request
 struct NodesServerStep {
+  static constexpr bool kKeepsState = true;
+  bool inline_act;
   __device__ __forceinline__ int t() const { return s_srv_req[0]; }
   __device__ __forceinline__ int flags() const { return s_srv_req[1]; }
   __device__ __forceinline__ uint32_t episode() const { return static_cast<uint32_t>(s_srv_req[2]); }
+  __device__ __forceinline__ const float* act(const ScArgs& x) const { return inline_act ? s_srv_act : x.act; }
+  __device__ __forceinline__ bool keep_state() const { return s_srv_req[4] != 0; }
 };
 
 template <int MAXD>
@@ -456,24 +476,37 @@ __global__ __launch_bounds__(64 * kNodesMaxWaves) void sc_nodes_server_kernel(co
   uint32_t last = __hip_atomic_load(&box->done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   uint32_t ex = exit_seen;
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  // wave 0: whether the LDS holds an env state this block stepped, and that step's episode
+  // and time (a request for the next time of the same episode finds its state there)
+  bool have = false;
+  uint32_t last_ep = 0;
+  int32_t last_t = 0;
   for (;;) {
     if (w == 0) {
-      const uint32_t v = lane0 < 16 ? __hip_atomic_load(line + lane0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+      // the request (line 0) and the inline action row (line 1) in one load, with the exit word
+      const uint32_t v = lane0 < 32 ? __hip_atomic_load(line + lane0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
       ex = __hip_atomic_load(&box->exit_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      uint32_t q[16];
+      uint32_t q[32];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) q[i] = __builtin_amdgcn_readlane(v, i);
+      for (int i = 0; i < 32; ++i) q[i] = __builtin_amdgcn_readlane(v, i);
       int cmd = 0;
       if (ex != exit_seen) {
         cmd = 2;
       } else if (q[0] != last && q[7] == mailbox_check(q)) {
-        cmd = 1;
+        cmd = (q[5] & 1u) ? 3 : 1;  // 3: a step whose action row came in line 1
         last = q[0];
+        const int32_t t = static_cast<int32_t>(q[2]);
+        const bool keep = have && !(q[5] & 2u) && q[4] == last_ep && t == last_t + 1;
         if (lane0 == 0) {
-          s_srv_req[0] = static_cast<int32_t>(q[2]);
+          s_srv_req[0] = t;
           s_srv_req[1] = static_cast<int32_t>(q[3]);
           s_srv_req[2] = static_cast<int32_t>(q[4]);
+          s_srv_req[4] = keep ? 1 : 0;
         }
+        if (lane0 >= 16 && lane0 < 32) s_srv_act[lane0 - 16] = __uint_as_float(v);
+        have = true;
+        last_ep = q[4];
+        last_t = t;
       } else if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
         cmd = 2;
       }
@@ -490,7 +523,7 @@ __global__ __launch_bounds__(64 * kNodesMaxWaves) void sc_nodes_server_kernel(co
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     int lane;
     asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
-    sc_nodes_tile<MAXD, true, false>(a, 0, lane, w, W, E, NodesServerStep{});
+    sc_nodes_tile<MAXD, true, false>(a, 0, lane, w, W, E, NodesServerStep{cmd == 3});
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every lane's stores before the answer
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&box->done_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -623,7 +656,7 @@ int sc_launch_nodes_server(const ScArgs& a, int maxd_bucket, int W, int E, hipSt
   if (W < 1 || W > kNodesMaxWaves) return fail(SCG_ERR_INVALID, "node-parallel server: %d waves per block", W);
   if (!a.obs_f64 || a.led_v) return fail(SCG_ERR_INVALID, "the SupplyChain step server runs float64 observations, no ledgers");
   const size_t lds = sc_nodes_lds_bytes(a.c.n_nodes, a.c.P, a.c.H, E, W, a.c.A, a.c.O, 8);
-  const size_t cap = sc_nodes_lds_max() - sizeof(s_srv_req);
+  const size_t cap = sc_nodes_lds_max() - 1024;  // room for the static request words and action row
   if (lds > cap) return fail(SCG_ERR_INVALID, "node-parallel server: %zu B of LDS per block", lds);
   static std::atomic<bool> raised[3][64] = {};
   int dev = 0;

@@ -908,8 +908,10 @@ __attribute__((visibility("default"))) int scg_sc_debug_stamps(unsigned long lon
 #endif
 
 // ---- step server (include/scgpu.h scg_sc_server_*) --------------------------------------
-static_assert(sizeof(scg_sc_server_box) == 128 && offsetof(scg_sc_server_box, done_seq) == 64, "SupplyChain mailbox");
-static_assert(sizeof(scg_sc_server) == 96, "SupplyChain server struct");
+static_assert(sizeof(scg_sc_server_box) == 192 && offsetof(scg_sc_server_box, action) == 64 &&
+                  offsetof(scg_sc_server_box, done_seq) == 128,
+              "SupplyChain mailbox");
+static_assert(sizeof(scg_sc_server) == 104, "SupplyChain server struct");
 static int sc_server_stop_now(scg_sc_server* sv) {
   if (!sv->running) return SCG_OK;
   __atomic_store_n(&sv->box_host->exit_req, sv->box_host->exit_req + 1, __ATOMIC_RELEASE);
@@ -961,15 +963,21 @@ int scg_sc_server_post(const scg_sc_config* cfg, scg_sc_state* st, scg_sc_server
   // a block idle for more than half its time-out may be exiting: retire it before posting
   if (sv->running && mono_ns() - sv->last_ns > static_cast<int64_t>(sv->idle_us) * 500)
     if (int rc = sc_server_stop_now(sv)) return rc;
-  uint32_t line[16] = {0};
+  // the request line and the inline action row: one env of at most 16 actions travels in
+  // the request, so the block does not read it across PCIe
+  uint32_t line[32] = {0};
   const uint32_t seq = sv->seq + 1;
+  const bool inline_act = sv->action_host && st->n_envs == 1 && cfg->n_actions <= 16;
   line[0] = seq;
   line[2] = static_cast<uint32_t>(t);
   line[3] = t == T ? 1u : 0u;
   line[4] = st->episode;
+  line[5] = (inline_act ? 1u : 0u) | (sv->reload ? 2u : 0u);
+  if (inline_act) std::memcpy(&line[16], sv->action_host, sizeof(float) * cfg->n_actions);
   line[7] = mailbox_check(line);
+  sv->reload = 0;
   uint32_t* dst = reinterpret_cast<uint32_t*>(b);
-  for (int i = 1; i < 16; ++i) __atomic_store_n(&dst[i], line[i], __ATOMIC_RELAXED);
+  for (int i = 1; i < 32; ++i) __atomic_store_n(&dst[i], line[i], __ATOMIC_RELAXED);
   __atomic_store_n(&dst[0], seq, __ATOMIC_RELEASE);
   sv->seq = seq;
   sv->t = t;

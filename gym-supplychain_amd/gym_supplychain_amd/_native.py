@@ -141,18 +141,20 @@ class BgServerSlot(ctypes.Structure):
 class ScServerBox(ctypes.Structure):
     """scg_sc_server_box (include/scgpu.h): the SupplyChain step server's mailbox."""
     _fields_ = [("req_seq", ctypes.c_uint32), ("cmd", ctypes.c_int32), ("t", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("episode", ctypes.c_uint32), ("pad0", ctypes.c_int32 * 2), ("check", ctypes.c_uint32),
-                ("pad1", ctypes.c_int32 * 8), ("done_seq", ctypes.c_uint32), ("exit_req", ctypes.c_uint32),
-                ("exit_seq", ctypes.c_uint32), ("pad2", ctypes.c_uint32 * 13)]
+                ("episode", ctypes.c_uint32), ("opts", ctypes.c_uint32), ("pad0", ctypes.c_int32),
+                ("check", ctypes.c_uint32), ("pad1", ctypes.c_int32 * 8), ("action", ctypes.c_float * 16),
+                ("done_seq", ctypes.c_uint32), ("exit_req", ctypes.c_uint32), ("exit_seq", ctypes.c_uint32),
+                ("pad2", ctypes.c_uint32 * 13)]
 
 
 class ScServer(ctypes.Structure):
     """scg_sc_server (include/scgpu.h): the SupplyChain step server of one drop-in env."""
     _fields_ = [("box_host", ctypes.c_void_p), ("box_dev", ctypes.c_void_p), ("stream", ctypes.c_void_p),
-                ("action", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p),
-                ("idle_us", ctypes.c_int32), ("check_us", ctypes.c_int32), ("running", ctypes.c_int32),
-                ("seq", ctypes.c_uint32), ("t", ctypes.c_int32), ("done", ctypes.c_int32), ("last_ns", ctypes.c_int64),
-                ("launches", ctypes.c_int64), ("relaunches", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("action", ctypes.c_void_p), ("action_host", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+                ("reward", ctypes.c_void_p), ("idle_us", ctypes.c_int32), ("check_us", ctypes.c_int32),
+                ("reload", ctypes.c_int32), ("running", ctypes.c_int32), ("seq", ctypes.c_uint32), ("t", ctypes.c_int32),
+                ("done", ctypes.c_int32), ("relaunches", ctypes.c_int32), ("last_ns", ctypes.c_int64),
+                ("launches", ctypes.c_int64)]
 
 
 # scg_bg_slab_field: word offsets of a BeerGame state slab (scg_bg_slab_layout)

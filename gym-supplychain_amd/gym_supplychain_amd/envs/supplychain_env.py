@@ -653,13 +653,13 @@ class _ScStepServer:
 
     IDLE_US = 20000
 
-    def __init__(self, vec, act_dev, obs_dev, rew_dev):
+    def __init__(self, vec, act_dev, act_host, obs_dev, rew_dev):
         stream, self.priority = resident.server_stream(vec.device)
         self._dev_index = vec._dev_index
         self._device = vec.device
         self._box = box = nat.MappedBuffer(ctypes.sizeof(nat.ScServerBox))
         self.box = nat.ScServerBox.from_address(box.host)
-        self.sv = nat.ScServer(box.host, box.dev, stream, act_dev, obs_dev, rew_dev, self.IDLE_US, 0)
+        self.sv = nat.ScServer(box.host, box.dev, stream, act_dev, act_host, obs_dev, rew_dev, self.IDLE_US, 0)
         self._args = (vec._cfg_addr, vec._st_addr, ctypes.addressof(self.sv))
         self._fast = nat.fast.sc_server_step
         self._closed = False
@@ -803,7 +803,8 @@ class SupplyChainEnv(spaces.Env):
         # synchronisation per step. SCG_SC_SERVER=0: one launch plus one synchronisation.
         self._server = None
         if os.environ.get("SCG_SC_SERVER", "1") != "0" and self._vec.kernel == "nodes" and not self.build_info:
-            self._server = _ScStepServer(self._vec, *self._io_ptrs)
+            act, obs, rew = self._io_ptrs
+            self._server = _ScStepServer(self._vec, act, io.host, obs, rew)
 
     @property
     def time_step(self):

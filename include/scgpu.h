@@ -546,19 +546,27 @@ SCG_API int scg_sc_draw_tables(const scg_sc_config* cfg, const scg_sc_state* st,
  * posted step, on the state and buffers the launch arguments named when it started — the
  * config's kernel must be SCG_SC_KERNEL_NODES, float64 observations, no ledgers, up to 64
  * envs. The same protocol as the BeerGame server: post the step (its time, flags and
- * episode travel in the request line), wait for the answer word; the block exits on
- * scg_sc_server_stop or after idle_us without a request, and the next post launches it
- * again (with the then-current state pointers and action / obs / reward buffers).
+ * episode travel in the request, and one env's action row too), wait for the answer word;
+ * the block exits on scg_sc_server_stop or after idle_us without a request, and the next post
+ * launches it again (with the then-current state pointers and action / obs / reward
+ * buffers). Between two steps of an episode the block keeps the env's state in its LDS (it
+ * still writes every step's state back to memory), so a step reads no state from memory;
+ * a reset (a new episode) or `reload` makes it read the state again.
  */
-typedef struct scg_sc_server_box { /* host-mapped (hipHostMalloc mapped + coherent), 128 B */
+typedef struct scg_sc_server_box { /* host-mapped (hipHostMalloc mapped + coherent), 192 B */
+  /* the request: two 64-byte lines, which the block reads in one load */
   uint32_t req_seq;   /* request number                                                   */
   int32_t cmd;        /* 0: step                                                          */
   int32_t t;          /* the step's time (1..T)                                           */
   int32_t flags;      /* bit0 terminal (as scg_sc_step's kernel flags)                    */
   uint32_t episode;   /* the state's episode                                              */
-  int32_t pad0[2];
-  uint32_t check;     /* scg mixing hash of the line's other 15 words                     */
+  uint32_t opts;      /* bit0: env 0's action row travels in action[] (one env, A <= 16);
+                         bit1: read the state from memory (not the block's LDS copy)      */
+  int32_t pad0;
+  uint32_t check;     /* scg mixing hash of the two lines' other 31 words                 */
   int32_t pad1[8];
+  float action[16];   /* line 1: the inline action row                                    */
+  /* the answer, on its own line */
   uint32_t done_seq;  /* the last request served (written by the block)                   */
   uint32_t exit_req;  /* the block exits when this differs from its launch value          */
   uint32_t exit_seq;  /* written by the block as it exits: the exit_req it saw last       */
@@ -570,19 +578,23 @@ typedef struct scg_sc_server {
   scg_sc_server_box* box_dev;  /* its device address                                      */
   void* stream;                /* a non-blocking stream of the caller's (high priority)   */
   const float* action;         /* DEVICE-visible float32 [N][A]                           */
+  const float* action_host;    /* its host address, or NULL: with one env of A <= 16 the
+                                  row is copied into the request (no read across PCIe)   */
   void* obs;                   /* DEVICE-visible float64 [N][O]                           */
   double* reward;              /* DEVICE-visible float64 [N]                              */
   int32_t idle_us;             /* the block exits after this long without a request       */
   int32_t check_us;            /* a waiting step checks this often for a gone block (0: 2 s) */
+  int32_t reload;              /* set by the caller when something else wrote the state (it
+                                  has no launch of its own on it otherwise): the next post
+                                  makes the block read it from memory; cleared by the post */
   /* host bookkeeping: zero before first use */
   int32_t running;
   uint32_t seq;                /* the request last posted                                 */
   int32_t t;                   /* the step it runs                                        */
   int32_t done;                /* that step is the terminal one                           */
+  int32_t relaunches;          /* blocks a wait launched again (block gone)               */
   int64_t last_ns;
   int64_t launches;
-  int32_t relaunches;
-  int32_t pad;
 } scg_sc_server;
 
 /* Post step(action) of the st->n_envs <= 64 envs (launches the block if needed). */

@@ -364,5 +364,5 @@ def test_server_struct_layouts_match_the_library():
     assert ctypes.sizeof(nat.BgServerBox) == 17 * 64 + 64 + nat.BG_SERVER_SLOTS * nat.BG_SERVER_ARGS_BYTES
     assert nat.BgServerBox.done_seq.offset == 16 * 64 and nat.BgServerBox.args.offset == 18 * 64
     assert ctypes.sizeof(nat.BgServer) == 72 and ctypes.sizeof(nat.BgServerSlot) == 64
-    assert ctypes.sizeof(nat.ScServerBox) == 128 and nat.ScServerBox.done_seq.offset == 64
-    assert ctypes.sizeof(nat.ScServer) == 96
+    assert ctypes.sizeof(nat.ScServerBox) == 192 and nat.ScServerBox.action.offset == 64
+    assert nat.ScServerBox.done_seq.offset == 128 and ctypes.sizeof(nat.ScServer) == 104

@@ -307,8 +307,11 @@ def test_nodes_kernel_persistent_tiles_equal_lane_kernel(scenario, kw, n_envs, m
     """The node-parallel kernel's persistent grid (scg_sc_nodes_max_blocks caps it, so a
     block steps several 64-env tiles in turn) against the lane kernel over every env, two
     episodes with auto-reset, with a 4- or 2-env tail tile; stochastic lead times, two
-    products with ledgers (that instantiation keeps one block per tile), and every env on
-    the serial walk — identical obs, rewards, returns, stocks, heaps and ledgers."""
+    products with ledgers, and every env on the serial walk — identical obs, rewards,
+    returns, stocks, heaps and ledgers. The cap applies to the ledger instantiation too, so
+    with max_blocks 2 or 3 this test deliberately runs its tile loop over several tiles per
+    block, which production never does (that instantiation keeps one block per tile,
+    SCG_NODES_LED_PERSISTENT=0); max_blocks 0 is the production grid."""
     import gym_supplychain_amd as gsa
     from gym_supplychain_amd import _native as nat
     kw = dict(kw)
