@@ -560,9 +560,6 @@ __global__ __launch_bounds__(kBlock) void bg_step_kernel(int32_t* __restrict__ i
 // A request is one 64-byte line of the mailbox (scg_bg_server_line, scg_mailbox.h).
 inline __host__ __device__ uint32_t server_line_check(const uint32_t (&w)[16]) { return mailbox_check(w); }
 
-#ifndef SCG_BG_SERVER_ARGS_SGPR
-#define SCG_BG_SERVER_ARGS_SGPR 0
-#endif
 constexpr int kServerBlock = 64;
 constexpr int kServerSlots = SCG_BG_SERVER_SLOTS;
 constexpr int kServerArgWords = (sizeof(BgArgs) + 15) / 16 * 4;  // rows 16-byte aligned
@@ -627,16 +624,7 @@ __global__ __launch_bounds__(kServerBlock) void bg_server_kernel(scg_bg_server_b
         __syncthreads();
         if (lane == 0) s_gen[slot] = w[6];
       }
-#if SCG_BG_SERVER_ARGS_SGPR
-      // the slot's arguments into scalar registers (one readfirstlane per word), so the week
-      // body addresses the state from SGPRs as the batch kernels do
-      BgArgs a;
-#pragma unroll
-      for (int k = 0; k < static_cast<int>(sizeof(BgArgs) / 4); ++k)
-        reinterpret_cast<uint32_t*>(&a)[k] = __builtin_amdgcn_readfirstlane(s_args[slot][k]);
-#else
       const BgArgs& a = *reinterpret_cast<const BgArgs*>(s_args[slot]);
-#endif
       WeekInfo wk{};
       wk.week = static_cast<int32_t>(w[3]);
       wk.demand_fixed = static_cast<int32_t>(w[4]);

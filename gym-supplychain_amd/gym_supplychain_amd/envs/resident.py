@@ -11,7 +11,6 @@ BeerGameEnv of a level count from one wave, so envs of one kind stepped in turn 
 switch; only stepping different kinds in turn costs a stop and a launch per switch.
 """
 import ctypes
-import os
 import threading
 
 import torch
@@ -49,8 +48,6 @@ def server_stream(device):
     with torch.cuda.device(device):
         least, greatest = ctypes.c_int(0), ctypes.c_int(0)
         if hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest)) != 0:
-            greatest.value = 0
-        if os.environ.get("SCG_SERVER_PRIORITY", "high") == "normal":  # A/B only
             greatest.value = 0
         if hip.hipStreamCreateWithPriority(ctypes.byref(stream), 1, greatest.value) != 0:  # hipStreamNonBlocking
             raise RuntimeError("hipStreamCreateWithPriority failed")
