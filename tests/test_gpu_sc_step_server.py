@@ -139,3 +139,44 @@ def test_sc_device_synchronize_after_a_step_is_bounded(monkeypatch):
     assert max(times) < 25e-3, times
     srv.close()
     ref.close()
+
+
+def test_sc_server_with_several_envs_through_the_c_abi():
+    """scg_sc_server_step serves up to 64 envs: a 5-env sc-2perstage batch (node-parallel
+    kernel, float64 observations) through the server, its actions read from device memory
+    and its state kept in the block's LDS between steps, equals a twin stepped by vec.step(),
+    over two episodes (the reset between them makes the block read the state again)."""
+    import ctypes
+    import gym_supplychain_amd as gsa
+    from gym_supplychain_amd import _native as nat
+    from gym_supplychain_amd.envs import resident
+    N, T = 5, 12
+    kw = dict(seed=4, device="cuda", kernel="nodes", obs_dtype=torch.float64, auto_reset=False, total_time_steps=T)
+    a = gsa.make_vec("sc-2perstage-v0", N, **kw)
+    b = gsa.make_vec("sc-2perstage-v0", N, **kw)
+    A, O = a.n_actions, a.spec.n_obs
+    act = torch.zeros((N, A), dtype=torch.float32, device="cuda")
+    obs = torch.zeros((N, O), dtype=torch.float64, device="cuda")
+    rew = torch.zeros((N,), dtype=torch.float64, device="cuda")
+    stream, _ = resident.server_stream(torch.device("cuda"))
+    box = nat.MappedBuffer(ctypes.sizeof(nat.ScServerBox))
+    sv = nat.ScServer(box.host, box.dev, stream, act.data_ptr(), None, obs.data_ptr(), rew.data_ptr(), 20000, 0)
+    done = ctypes.c_int32(0)
+    gen = torch.Generator(device="cuda").manual_seed(8)
+    try:
+        for ep in range(2):
+            assert torch.equal(a.reset(), b.reset())
+            torch.cuda.synchronize()
+            for t in range(T):
+                x = torch.rand((N, A), generator=gen, device="cuda") * 2 - 1
+                act.copy_(x)
+                torch.cuda.synchronize()
+                nat.check(nat.lib.scg_sc_server_step(ctypes.byref(a._cfg), ctypes.byref(a._st), ctypes.byref(sv),
+                                                     ctypes.byref(done)))
+                o, r, d, _ = b.step(x)
+                assert torch.equal(obs, o) and torch.equal(rew, r), (ep, t)
+                assert bool(done.value) == bool(d.all()), (ep, t)
+            assert torch.equal(a.stock, b.stock), ep
+    finally:
+        nat.check(nat.lib.scg_sc_server_stop(ctypes.byref(sv)))
+        resident.destroy_stream(stream)

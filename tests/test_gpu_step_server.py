@@ -263,3 +263,44 @@ def test_dropin_envs_stepped_from_threads(monkeypatch):
             assert np.array_equal(o, o1) and r == r1 and d == d1, (k, w)
         ref.close()
         envs[k].close()
+
+
+def test_server_slot_with_several_envs_through_the_c_abi():
+    """A slot serves up to 64 envs (include/scgpu.h scg_bg_server_*): a 5-env BeerGameVecEnv
+    (separate state buffers) stepped through scg_bg_server_step, its action row read from
+    device memory (no inline row), equals a twin stepped by vec.step(), week for week."""
+    import ctypes
+    from gym_supplychain_amd import BeerGameVecEnv
+    from gym_supplychain_amd import _native as nat
+    from gym_supplychain_amd.envs import resident
+    T, L, N = 20, 4, 5
+    info = _info(L, T, 21)
+    a = BeerGameVecEnv(N, info, demand="fixed", device="cuda", auto_reset=False, state_slab=False)
+    b = BeerGameVecEnv(N, info, demand="fixed", device="cuda", auto_reset=False, state_slab=False)
+    act = torch.zeros((N, L), dtype=torch.int32, device="cuda")
+    obs = torch.zeros((N, L), dtype=torch.int32, device="cuda")
+    rew = torch.zeros((N,), dtype=torch.int32, device="cuda")
+    stream, _ = resident.server_stream(torch.device("cuda"))
+    box = nat.MappedBuffer(ctypes.sizeof(nat.BgServerBox))
+    sv = nat.BgServer(box.host, box.dev, stream, L, nat.SCG_DEMAND_FIXED, 20000, 0)
+    slot = nat.BgServerSlot(None, act.data_ptr(), None, obs.data_ptr(), rew.data_ptr(), -1)
+    nat.check(nat.lib.scg_bg_server_attach(ctypes.byref(sv), ctypes.byref(slot)))
+    done = ctypes.c_int32(0)
+    try:
+        assert torch.equal(a.reset(), b.reset())
+        torch.cuda.synchronize()
+        gen = torch.Generator(device="cuda").manual_seed(3)
+        for w in range(T):
+            x = torch.randint(0, 15, (N, L), generator=gen, device="cuda", dtype=torch.int32)
+            act.copy_(x)
+            torch.cuda.synchronize()  # the row is in place before the post
+            nat.check(nat.lib.scg_bg_server_step(ctypes.byref(a._cfg), ctypes.byref(a._st), ctypes.byref(slot),
+                                                 ctypes.byref(done)))
+            o, r, d, _ = b.step(x)
+            assert torch.equal(obs, o) and torch.equal(rew, r), w
+            assert bool(done.value) == bool(d.all()) and a.week == b.week == w + 1
+        assert torch.equal(a.inventory, b.inventory) and torch.equal(a.backlog, b.backlog)
+    finally:
+        nat.check(nat.lib.scg_bg_server_detach(ctypes.byref(slot)))
+        nat.check(nat.lib.scg_bg_server_stop(ctypes.byref(sv)))
+        resident.destroy_stream(stream)
