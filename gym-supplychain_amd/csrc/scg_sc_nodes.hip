@@ -378,7 +378,8 @@ __device__ __forceinline__ void sc_nodes_tile(const ScArgs& a, int64_t tile, int
   TileWalk tw(threadIdx.x, blockDim.x, c.O);
   for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
     const ObsT x = obs_t[tw.r * Op + tw.k];
-    if constexpr (kStream) {
+    // (the step server's rows go to host-mapped memory: plain stores there)
+    if constexpr (kStream && !Step::kKeepsState) {
       if (dst0) __builtin_nontemporal_store(x, &dst0[n0 * c.O + q]);
       if (dst1) __builtin_nontemporal_store(x, &dst1[n0 * c.O + q]);
     } else {
@@ -450,8 +451,9 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
 // puts what it found in LDS; after a barrier every wave either exits, sleeps and polls again,
 // or runs tile 0 of the step with the request's time, flags, episode and action row
 // (NodesServerStep) — the batch kernel's code, minus the state loads when the block's LDS
-// still holds the state of this env's previous step — and then lane 0 publishes the request
-// number with a system-scope release store. At launch the
+// still holds the state of this env's previous step — and then, past a barrier, thread 0
+// publishes the request number with a system-scope release store (wave 0 acquired when it
+// found the request: one cache invalidation and one L2 write-back per step for the block). At launch the
 // last request served is the answer word, so a request posted while no block ran is served
 // first. It exits when exit_req changes or after idle_ticks of the 100 MHz real-time clock
 // without a request, and writes the exit word it saw as it goes.
@@ -504,6 +506,9 @@ __global__ __launch_bounds__(64 * kNodesMaxWaves) void sc_nodes_server_kernel(co
           s_srv_req[4] = keep ? 1 : 0;
         }
         if (lane0 >= 16 && lane0 < 32) s_srv_act[lane0 - 16] = __uint_as_float(v);
+        // the acquire for the whole block: one wave's invalidation of the CU's caches and the
+        // L2 serves every wave, which the barrier below orders after it
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         have = true;
         last_ep = q[4];
         last_t = t;
@@ -520,11 +525,12 @@ __global__ __launch_bounds__(64 * kNodesMaxWaves) void sc_nodes_server_kernel(co
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     int lane;
     asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
     sc_nodes_tile<MAXD, true, false>(a, 0, lane, w, W, E, NodesServerStep{cmd == 3});
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every lane's stores before the answer
+    // every wave's stores happen before thread 0's system-scope release store through the
+    // barrier, so one write-back of the L2 (the store's release) publishes them all; a fence in
+    // each of the W waves would write the L2 back W times (2.5 us per step for W = 8)
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&box->done_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     t0 = __builtin_amdgcn_s_memrealtime();
