@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstring>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -459,6 +460,14 @@ void sc_step_nodes_kernel(const ScArgs a_arg, int W, int E) {
 // without a request, and writes the exit word it saw as it goes.
 __shared__ int32_t s_srv_req[5];  // t, flags, episode, command (0 none, 1 / 3 step, 2 exit), keep
 __shared__ float s_srv_act[16];   // env 0's action row when it travelled in the request
+#ifdef SCG_NODES_STAMPS
+// Diagnostic build only (tools/sc_server_phase_probe.py): per wave, the shader clocks of each
+// phase of every served step summed — [0] request seen -> tile start, then the tile's phases
+// in order (stamps 0 -> 5 -> 6 -> 1 -> 2 -> 3 -> 7 -> 4), [8] tile end -> past the closing
+// barrier, [9] the steps served — read without a device sync by scg_sc_server_debug_phases.
+__device__ unsigned long long g_srv_phases[kNodesMaxWaves][10];
+__shared__ unsigned long long s_srv_seen;
+#endif
 struct NodesServerStep {
   static constexpr bool kKeepsState = true;
   bool inline_act;
@@ -509,6 +518,9 @@ __global__ __launch_bounds__(64 * kNodesMaxWaves) void sc_nodes_server_kernel(co
         // the acquire for the whole block: one wave's invalidation of the CU's caches and the
         // L2 serves every wave, which the barrier below orders after it
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#ifdef SCG_NODES_STAMPS
+        if (lane0 == 0) s_srv_seen = __builtin_amdgcn_s_memtime();
+#endif
         have = true;
         last_ep = q[4];
         last_t = t;
@@ -532,6 +544,20 @@ __global__ __launch_bounds__(64 * kNodesMaxWaves) void sc_nodes_server_kernel(co
     // barrier, so one write-back of the L2 (the store's release) publishes them all; a fence in
     // each of the W waves would write the L2 back W times (2.5 us per step for W = 8)
     __syncthreads();
+#if defined(SCG_NODES_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+    {
+      const unsigned long long past = __builtin_amdgcn_s_memtime();
+      const unsigned long long* l_ = s_nodes_stamps + w * kNLdsSlots;
+      if (lane0 == 0 && w < kNodesMaxWaves) {
+        const int order[8] = {0, 5, 6, 1, 2, 3, 7, 4};
+        unsigned long long* acc = g_srv_phases[w];
+        acc[0] += l_[0] - s_srv_seen;
+        for (int k = 1; k < 8; ++k) acc[k] += l_[order[k]] - l_[order[k - 1]];
+        acc[8] += past - l_[4];
+        acc[9] += 1;
+      }
+    }
+#endif
     if (threadIdx.x == 0) __hip_atomic_store(&box->done_seq, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     t0 = __builtin_amdgcn_s_memrealtime();
   }
@@ -662,7 +688,7 @@ int sc_launch_nodes_server(const ScArgs& a, int maxd_bucket, int W, int E, hipSt
   if (W < 1 || W > kNodesMaxWaves) return fail(SCG_ERR_INVALID, "node-parallel server: %d waves per block", W);
   if (!a.obs_f64 || a.led_v) return fail(SCG_ERR_INVALID, "the SupplyChain step server runs float64 observations, no ledgers");
   const size_t lds = sc_nodes_lds_bytes(a.c.n_nodes, a.c.P, a.c.H, E, W, a.c.A, a.c.O, 8);
-  const size_t cap = sc_nodes_lds_max() - 1024;  // room for the static request words and action row
+  const size_t cap = sc_nodes_lds_max() - kNodesStaticLds - 1024;  // room for the static request words and action row
   if (lds > cap) return fail(SCG_ERR_INVALID, "node-parallel server: %zu B of LDS per block", lds);
   static std::atomic<bool> raised[3][64] = {};
   int dev = 0;
@@ -702,5 +728,33 @@ extern "C" __attribute__((visibility("default"))) int scg_nodes_debug_stamps(uns
       hipSuccess)
     return scg::fail(SCG_ERR_HIP, "stamp copy");
   return SCG_OK;
+}
+
+// Diagnostic build only: the step server's per-wave phase sums (g_srv_phases) to host memory
+// (8 x 10 words), on a stream of its own, without waiting for the resident server block;
+// reset != 0 clears them afterwards.
+extern "C" __attribute__((visibility("default"))) int scg_sc_server_debug_phases(unsigned long long* host, int reset) {
+  (void)hipGetLastError();  // an error an earlier call left behind is not this probe's
+  static unsigned long long* pinned = nullptr;
+  if (!pinned && hipHostMalloc(reinterpret_cast<void**>(&pinned), sizeof(scg::g_srv_phases), 0) != hipSuccess)
+    return scg::fail(SCG_ERR_HIP, "phase probe: pinned buffer");
+  void* dev = nullptr;
+  if (hipGetSymbolAddress(&dev, HIP_SYMBOL(scg::g_srv_phases)) != hipSuccess) return scg::fail(SCG_ERR_HIP, "symbol");
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return scg::fail(SCG_ERR_HIP, "stream");
+  int rc = SCG_OK;
+  hipError_t e = hipMemcpyAsync(pinned, dev, sizeof(scg::g_srv_phases), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) rc = scg::fail(SCG_ERR_HIP, "phase copy: %s", hipGetErrorString(e));
+  if (rc == SCG_OK) {
+    std::memcpy(host, pinned, sizeof(scg::g_srv_phases));
+    if (reset) {
+      e = hipMemsetAsync(dev, 0, sizeof(scg::g_srv_phases), s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) rc = scg::fail(SCG_ERR_HIP, "phase reset: %s", hipGetErrorString(e));
+    }
+  }
+  (void)hipStreamDestroy(s);
+  return rc;
 }
 #endif

@@ -792,6 +792,7 @@ class SupplyChainEnv(spaces.Env):
         ra = (4 * A + 15) // 16 * 16
         self._io = io = nat.MappedBuffer(ra + 8 * O + 8)
         self._act_np = io.view(np.float32, 0, A).reshape(1, A)
+        self._act_row, self._n_act = self._act_np[0], A
         self._obs_np = io.view(np.float64, ra, O)
         self._rew_np = io.view(np.float64, ra + 8 * O, 1)
         self._io_ptrs = (io.dev, io.dev + ra, io.dev + ra + 8 * O)
@@ -852,14 +853,21 @@ class SupplyChainEnv(spaces.Env):
         return self.current_state
 
     def step(self, action):
-        a = np.asarray(action, dtype=np.float32).reshape(-1)
-        n = self._act_np.shape[1]
-        if a.size < n:  # the reference's per-node slices run past the end (:716-717 -> act)
-            raise IndexError(f"action has {a.size} values, the chain needs {n}")
-        self._act_np[0, :] = a[:n]  # like the reference, values beyond the chain's actions are unused
+        # (the per-call Python here is part of the step's latency: a float32 vector, the
+        # usual case, goes straight into the host-mapped action row)
+        a = action
+        if type(a) is not np.ndarray or a.dtype != np.float32 or a.ndim != 1:
+            a = np.asarray(a, dtype=np.float32).reshape(-1)
+        n = self._n_act
+        if a.size != n:
+            if a.size < n:  # the reference's per-node slices run past the end (:716-717 -> act)
+                raise IndexError(f"action has {a.size} values, the chain needs {n}")
+            a = a[:n]  # like the reference, values beyond the chain's actions are unused
+        self._act_row[:] = a
         v = self._vec
-        if self._server is not None:
-            r = self._server.step()  # returns once the block has written obs and reward
+        srv = self._server
+        if srv is not None:
+            r = srv.step()  # returns once the block has written obs and reward
             if r > 1:
                 nat.check(r >> 1)
         else:
@@ -871,16 +879,16 @@ class SupplyChainEnv(spaces.Env):
             rc = self._sync(stream)
             if rc:
                 raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
-        self.current_state = self._obs_np.copy()
-        self.current_reward = np.float64(self._rew_np[0])
-        self.episode_rewards += self.current_reward
-        if self.time_step == self.total_time_steps:
-            self._vec.check_errors()
-        info = {}
+        self.current_state = obs = self._obs_np.copy()
+        self.current_reward = rew = self._rew_np[0]  # an np.float64 (:734)
+        self.episode_rewards += rew
+        done = v._st.time_step == self.total_time_steps
+        if done:
+            v.check_errors()
         if self.build_info:
-            self.est_episode.update(self._vec.sc_episode(0))
-            info = {"sc_episode": self.est_episode}
-        return self.current_state, self.current_reward, self.time_step == self.total_time_steps, info
+            self.est_episode.update(v.sc_episode(0))
+            return obs, rew, done, {"sc_episode": self.est_episode}
+        return obs, rew, done, {}
 
     @property
     def stock(self):

@@ -58,6 +58,30 @@ def test_sc_step_server_matches_launch_path(monkeypatch):
     ref.close()
 
 
+def test_sc_step_action_forms(monkeypatch):
+    """step() takes the action as the reference does (:704, :716-717): any array-like of at
+    least n_actions values, cast to float32, the rest unused; fewer raise IndexError. A list,
+    a float64 array, a (1, A) array and a longer array step exactly as the float32 vector does
+    (the facade's fast path), on the server and the launch path."""
+    srv, ref = _pair(monkeypatch, T=12, seed=4)
+    rng = np.random.RandomState(2)
+    A = srv.action_space.shape[0]
+    srv.reset()
+    ref.reset()
+    for t in range(12):
+        a64 = rng.uniform(-1, 1, A + 3)
+        forms = [a64[:A].tolist(), a64[:A], a64[:A].reshape(1, A), a64.astype(np.float32)]
+        o1, r1, d1, _ = srv.step(forms[t % 4])
+        o2, r2, d2, _ = ref.step(a64[:A].astype(np.float32))
+        assert np.array_equal(o1, o2) and r1 == r2 and d1 == d2, t
+        assert type(r1) is np.float64 and o1.dtype == np.float64
+    for env in (srv, ref):
+        env.reset()
+        with pytest.raises(IndexError):
+            env.step(np.zeros(A - 1, dtype=np.float32))
+        env.close()
+
+
 def test_sc_server_full_episode_and_terminal(monkeypatch):
     """A whole 360-step sc-2perstage episode (the terminal step's flags travel in the request)."""
     srv, ref = _pair(monkeypatch, T=360, seed=3)
