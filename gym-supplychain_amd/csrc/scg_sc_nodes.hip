@@ -147,7 +147,8 @@ struct TileWalk {
 // Streaming (non-temporal) stores for the rows a step writes once and only the next step
 // reads (heap copy-back, stocks, observations): 0 off, 1 the ledger instantiation only, 2
 // every instantiation (sc-2perstage 37.4 -> 36.7 us; the ledger run within noise,
-// profiles/r05j_nodes_nt_ab.log).
+// profiles/r05j_nodes_nt_ab.log); write-through rather than non-temporal by SCG_NODES_WT
+// (scg_supplychain_nodes.h).
 #ifndef SCG_NODES_NT
 #define SCG_NODES_NT 2
 #endif
@@ -380,7 +381,10 @@ __device__ __forceinline__ void sc_nodes_tile(const ScArgs& a, int64_t tile, int
   for (int q = threadIdx.x; q < nb * c.O; q += blockDim.x, tw.next()) {
     const ObsT x = obs_t[tw.r * Op + tw.k];
     // (the step server's rows go to host-mapped memory: plain stores there)
-    if constexpr (kStream && !Step::kKeepsState) {
+    if constexpr (kStream && !Step::kKeepsState && SCG_NODES_WT >= 2) {
+      if (dst0) __hip_atomic_store(&dst0[n0 * c.O + q], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (dst1) __hip_atomic_store(&dst1[n0 * c.O + q], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (kStream && !Step::kKeepsState) {
       if (dst0) __builtin_nontemporal_store(x, &dst0[n0 * c.O + q]);
       if (dst1) __builtin_nontemporal_store(x, &dst1[n0 * c.O + q]);
     } else {
@@ -402,7 +406,10 @@ __device__ __forceinline__ void sc_nodes_tile(const ScArgs& a, int64_t tile, int
                // next tile's stage rewrites these rows: the same wave)
     for (int i = w; i < NN; i += W)
       for (int p = 0; p < P; ++p) {
-        if constexpr (kStream)
+        if constexpr (kStream && SCG_NODES_WT >= 2)
+          __hip_atomic_store(&a.stock[(i * P + p) * a.n + n], stk[(i * P + p) * 64 + lane], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        else if constexpr (kStream)
           __builtin_nontemporal_store(stk[(i * P + p) * 64 + lane], &a.stock[(i * P + p) * a.n + n]);
         else
           a.stock[(i * P + p) * a.n + n] = stk[(i * P + p) * 64 + lane];

@@ -28,6 +28,15 @@
 
 #include "scg_supplychain_core.h"
 
+// The node-parallel kernel's streaming stores (the heap copy-back; at 2 also the stock and
+// observation rows of the batch kernel) as write-through stores (sc1: the line leaves the
+// L2 with the store instead of staying dirty until evicted or written back at the launch's
+// end): sc-2perstage 37.2-37.5 -> 35.7-37.0 us, the two-product chain 86-88 -> 82-84 us
+// (profiles/r06t_nodes_wt_ab*.log, r06u_*, r06v_*); 0 keeps the non-temporal stores.
+#ifndef SCG_NODES_WT
+#define SCG_NODES_WT 2
+#endif
+
 namespace scg {
 
 __host__ __device__ __forceinline__ int sc_ctz64(uint64_t m) { return __builtin_ctzll(m); }
@@ -195,8 +204,15 @@ __host__ __device__ inline void sc_nodes_heap(const ScCtx& c, ScEnv& g, const He
   sc_observe_bins(c, lh, sz, t, i, p, out, [&](int k, const HeapEntry& e) {  // copy back
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (kStream) {
+#if SCG_NODES_WT
+      // write-through (sc1): the line leaves the L2 now instead of staying dirty for the
+      // kernel's end-of-launch write-back
+      __hip_atomic_store(&gh.tk[k * gh.stride], e.tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gh.val[k * gh.stride], e.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
       __builtin_nontemporal_store(e.tk, &gh.tk[k * gh.stride]);
       __builtin_nontemporal_store(e.v, &gh.val[k * gh.stride]);
+#endif
       return;
     }
 #endif
